@@ -1,0 +1,256 @@
+"""bench.py — walker-timesteps/s of the batched ODE integrate + fused likelihood on MI355X.
+
+Contract (see task README): ``python bench.py --gpus N --steps K --warmup W``; N>1 is
+launched by torchrun, one rank per GPU.  One *step* = one batched integrate of the
+rank's walkers in trajectory mode (writes traj[T][S][W] fp64, the odeint [T,S] output
+of ODElib/Framework.py:656, plus the fused chi / R² residual of :685-706).
+
+Workload (BASELINE.json configs[1]): 4-state SEIV ``two_i``, 65 536
+walkers per GPU, fixed-step RK4, t = linspace(0, 3, 1000), y0 = demo data
+(S 5 236 900, V 10 981 000), θ_w = θ*·exp(0.05 z_w) with numpy RandomState(0),
+observations = demo data (H = S+I1+I2, V).  Walkers shard across ranks by contiguous
+global id with no data-path collective ("scaling": "weak"); an MCMC leg
+(device Metropolis–Hastings) ends with one RCCL all-gather of the posterior block.
+
+Roofline: HBM, algorithmic bytes per walker-timestep = 8·S (trajectory store),
+kernel time from HIP events recorded on the stream the kernel is launched on.
+cpu_baseline: the oracle's scipy-odeint restatement of Framework.py:656-697
+(oracle/cpu_ref.py) on the host cores, bounded sample, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+THETA_STAR = [7.475e-9, 1.069e-7, 19.73, 1.934, 2.799]  # twoI posterior medians (notebook:15120-15128)
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_VALU_TFS = 78.6     # MI355X FP64 vector spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
+    ap.add_argument("--model", default="two_i", help="two_i | chain<N>")
+    ap.add_argument("--method", default="rk4", choices=["rk4", "dopri5"])
+    ap.add_argument("--times", type=int, default=1000)
+    ap.add_argument("--cached-stores", action="store_true", help="plain (cached) trajectory stores")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mcmc-iters", type=int, default=21, help="MCMC leg iterations (0 = skip)")
+    return ap.parse_args()
+
+
+def build_problem(model: str, method: str, T: int):
+    """FitProblem for the bench workload (host-side set-up only)."""
+    import numpy as np
+    import pandas as pd
+    from odelib_amd import ModelFramework, parameter
+    from odelib_amd.models import BUILTIN, chain_rhs
+    df = pd.read_csv(os.path.join(ROOT, "tests", "golden", "demodata.csv")).replace({"virus": "V", "host": "H"})
+    if model == "two_i":
+        n, ode = 4, BUILTIN["two_i"][3]
+    elif model.startswith("chain"):
+        n = int(model[5:])
+        ode = chain_rhs(n)
+    else:
+        raise SystemExit(f"unknown bench model {model}")
+    snames = ["S"] + [f"I{k}" for k in range(1, n - 1)] + ["V"]
+    pn = ["mu", "phi", "beta", "lam", "tau"]
+    m = ModelFramework(ODE=ode, parameter_names=pn, state_names=snames, dataframe=df,
+                       state_summations={"H": snames[:-1]}, t_steps=T, S=5236900, method=method,
+                       device_model="two_i" if model == "two_i" else "chain",
+                       **{p: parameter(init_value=v) for p, v in zip(pn, THETA_STAR)})
+    return m, np.asarray(m.get_inits(), float)
+
+
+def synthetic_walkers(n_total: int, P: int):
+    import numpy as np
+    z = np.random.RandomState(0).standard_normal((P, n_total))
+    return np.asarray(THETA_STAR)[:, None] * np.exp(0.05 * z)
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle)
+def _cpu_worker(args):
+    model, times, wall_budget, theta_cols, y0, tidx, mask, O, Ssig = args
+    import numpy as np
+    from oracle import cpu_ref
+    from odelib_amd.models import BUILTIN, chain_rhs
+    ode = BUILTIN["two_i"][3] if model == "two_i" else chain_rhs(int(model[5:]))
+    S = len(y0)
+    done, t0 = 0, time.perf_counter()
+    for th in theta_cols:
+        traj = cpu_ref.odeint_traj(ode, y0, times, th)  # Framework.py:656
+        # summation + gather at pred_tindex + masked chi (Framework.py:659-697)
+        C = np.array([sum(traj[i, s] for s in range(S) if (int(mk) >> s) & 1) for i, mk in zip(tidx, mask)])
+        cpu_ref.chi(O, np.log(C), Ssig)
+        done += 1
+        if time.perf_counter() - t0 > wall_budget:
+            break
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(model, fp, y0, budget_s, P):
+    """Oracle (scipy odeint, the reference's integrator) on the host cores; fork-based
+    pool started before this process initialises the GPU."""
+    import multiprocessing as mp
+    cores = min(16, os.cpu_count() or 1)
+    theta = synthetic_walkers(cores * 16384, P)
+    jobs = [(model, fp.times, budget_s, [theta[:, w] for w in range(c, theta.shape[1], cores)], y0,
+             fp.obs_tidx, fp.obs_mask, fp.obs_log, fp.obs_logsigma) for c in range(cores)]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t0
+    walkers = sum(r[0] for r in res)
+    T = len(fp.times)
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": walkers * (T - 1) / wall, "unit": "walker-timesteps/s", "cores": cores, "kind": "port",
+            "sample": f"{walkers} walkers x {T - 1} intervals: scipy odeint (LSODA, default tol) + summation + "
+                      f"masked chi (oracle/cpu_ref.py), multiprocessing.Pool({cores}) for {wall:.1f} s wall; "
+                      f"CPU: {cpu_model}"}
+
+
+# ------------------------------------------------------------------ main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = world if world > 1 else args.gpus
+    P = 5
+
+    # host-side problem set-up, then the CPU baseline (forks before the GPU is touched)
+    m, y0h = build_problem(args.model, args.method, args.times)
+    fp_host = m.fit_problem()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.model, fp_host, y0h, args.cpu_seconds, P)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    eng = m.engine()
+    fp = eng.problem
+    S, T = fp.n_states, fp.n_times
+    Wl = args.walkers
+    theta_all = synthetic_walkers(Wl * n_gpus, P)
+    theta = torch.as_tensor(np.ascontiguousarray(theta_all[:, rank * Wl:(rank + 1) * Wl]), device=dev)
+    y0 = torch.as_tensor(np.repeat(y0h[:, None], Wl, axis=1), device=dev).contiguous()
+    traj = eng.empty_traj(Wl)
+
+    def step():
+        return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores, sync=False)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        out = step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    wts = n_gpus * Wl * (T - 1) * args.steps
+    value = wts / elapsed
+    bytes_launch = Wl * (T - 1) * 8 * S + Wl * 8 * (S + P + 2)  # traj + y0/θ/chi/ssres
+    achieved = bytes_launch / kern_avg_s / 1e9
+    chi_ok = bool(torch.isfinite(out["chi"]).all().item())
+
+    # ---- MCMC leg: device Metropolis–Hastings (RK4), posterior all-gather over RCCL ----
+    mcmc = None
+    if args.mcmc_iters > 1:
+        nits = args.mcmc_iters
+        burn = nits // 2
+        walk = np.ones(P, np.uint8)
+        torch.cuda.synchronize(dev)
+        tm0 = time.perf_counter()
+        r = eng.mh_run(theta, y0, nits=nits, burnin=burn, walk_mask=walk, rng="philox", seed=1234,
+                       walker_offset=rank * Wl)
+        torch.cuda.synchronize(dev)
+        t_mh = time.perf_counter() - tm0
+        mh_kernel_ms = eng.last_kernel_ms()
+        t_ag = 0.0
+        gathered_bytes = r["samples"].numel() * 8 * n_gpus
+        if world > 1:
+            blk = r["samples"].contiguous()
+            gath = torch.empty((world,) + tuple(blk.shape), dtype=blk.dtype, device=dev)
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+            ta = time.perf_counter()
+            dist.all_gather_into_tensor(gath, blk)
+            torch.cuda.synchronize(dev)
+            t_ag = time.perf_counter() - ta
+        if world > 1:
+            tt = torch.tensor([t_mh, t_ag], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t_mh, t_ag = float(tt[0]), float(tt[1])
+        mh_wts = n_gpus * Wl * (T - 1) * nits  # a-priori integrate + nits-1 proposals
+        flops_per_wts = 4 * 20 + 4 * 12  # 4 RHS x ~20 flop + RK update (4-state two_i)
+        mcmc = {"iterations": nits, "walker_timesteps_per_s": mh_wts / t_mh, "kernel_ms": mh_kernel_ms,
+                "fp64_tflops_est": Wl * (T - 1) * nits * flops_per_wts * (S / 4.0) / (mh_kernel_ms / 1e3) / 1e12,
+                "fp64_peak_tflops": FP64_VALU_TFS, "allgather_s": t_ag, "allgather_bytes": gathered_bytes,
+                "rng": "philox"}
+
+    if rank == 0:
+        line = {
+            "metric": "walker-timesteps/sec, 4-state infection ODE, 65536 walkers, 1/2/4/8 MI355X"
+            if args.model == "two_i" else f"walker-timesteps/sec, {S}-state chain ODE",
+            "value": value, "unit": "walker-timesteps/s", "n_gpus": n_gpus, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{args.model} {args.method} trajectory-mode integrate + fused chi",
+                       "walkers_per_gpu": Wl, "walkers_total": Wl * n_gpus, "states": S, "times": T,
+                       "method": args.method, "stores": "cached" if args.cached_stores else "nontemporal", "parallelism": f"walker-shard x{n_gpus}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel_ms": kern_avg_s * 1e3, "bytes_per_launch": bytes_launch},
+            "cpu_baseline": cpu,
+            "mcmc": mcmc,
+            "chi_finite": chi_ok,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,179 @@
+/*
+ * odelib_amd.h — C-ABI of the MI355X batched ODE-in-MCMC engine (libodelib_amd.so).
+ *
+ * This is the drop-in boundary for ODElib's parameter-fitting hot path.  The
+ * reference has no FFI: its boundary is Python.  Each entry point
+ * below replaces one reference call site; the Python host layer
+ * (odelib_amd/_native.py) binds them with ctypes exactly as a maintainer would
+ * from ODElib itself.
+ *
+ *   oe_problem_set   <- ModelFramework.__init__ data setup: times grid
+ *                       (ODElib/Framework.py:234), pred_tindex / obs arrays
+ *                       (Framework.py:309-329), state summations
+ *                       (Framework.py:332-381, applied at :659-664).
+ *   oe_integrate     <- ModelFramework.integrate (Framework.py:622-683): the
+ *                       scipy odeint call at Framework.py:656, fused with the
+ *                       observation gather (:677-682), get_chi
+ *                       (Framework.py:685-697 / Statistics/stats.py:22-41)
+ *                       and the Rsqrd residual (stats.py:49-56), for W walkers.
+ *   oe_mh_run        <- Statistics/Samplers.py:53-174 MetropolisHastings, for W
+ *                       independent chains (one per walker), i.e. the
+ *                       MCMC(...) chain loop of Framework.py:1013-1030.
+ *
+ * Conventions
+ *   - All buffers are caller-owned.  Pointers are DEVICE pointers unless the
+ *     call's flags contain OE_HOST_PTRS (then the library stages through its
+ *     own scratch).  The library never frees caller memory.
+ *   - Batched layouts are walker-minor ("[state][walker]"): element (s, w) of
+ *     a [S][W] array is at s*W + w, so 64 lanes of a wavefront touch 512
+ *     contiguous bytes.
+ *   - Every call returns OE_OK (0) or a negative OE_ERR_* code; the message is
+ *     read with oe_last_error().  Nothing throws or aborts across the ABI.
+ *   - Threading: one context per device per host thread.  Calls are
+ *     synchronous on return unless OE_ASYNC is passed (then ordered on the
+ *     context's stream, see oe_ctx_set_stream).
+ */
+#ifndef ODELIB_AMD_H
+#define ODELIB_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OE_ABI_VERSION 1
+
+/* return codes */
+enum {
+  OE_OK = 0,
+  OE_ERR_ARG = -1,         /* invalid argument / shape */
+  OE_ERR_HIP = -2,         /* HIP runtime error */
+  OE_ERR_STATE = -3,       /* no problem set, etc. */
+  OE_ERR_UNSUPPORTED = -4, /* model / method combination not compiled in */
+  OE_ERR_NOMEM = -5
+};
+
+/* integrators */
+enum {
+  OE_METHOD_RK4 = 0,   /* fixed-step classical RK4, rk4_substeps steps per output interval */
+  OE_METHOD_DOPRI5 = 1 /* Dormand–Prince 5(4), wavefront-shared step, max-norm error,
+                          dense output onto the times grid */
+};
+
+/* built-in right-hand sides (demo notebook models + synthetic chain) */
+enum {
+  OE_MODEL_ZERO_I = 0, /* S=2 (S,V),        P=3 (mu,phi,beta)         notebook zero_i */
+  OE_MODEL_ONE_I = 1,  /* S=3 (S,I1,V),     P=4 (mu,phi,beta,lam)     notebook one_i  */
+  OE_MODEL_TWO_I = 2,  /* S=4 (S,I1,I2,V),  P=5 (mu,phi,beta,lam,tau) notebook two_i  */
+  OE_MODEL_CHAIN = 3   /* S=N (S,I1..I_{N-2},V), P=5; N=4 reduces to two_i */
+};
+
+/* per-walker status bits (OR-ed) */
+enum {
+  OE_STATUS_NONFINITE = 1, /* a state became NaN/inf */
+  OE_STATUS_NEGATIVE = 2,  /* a state went negative at an output time */
+  OE_STATUS_MAXSTEP = 4    /* DOPRI5 step budget / step underflow: walker abandoned (NaN output) */
+};
+
+/* call flags */
+enum {
+  OE_HOST_PTRS = 1u, /* buffers are host memory */
+  OE_ASYNC = 2u,     /* do not synchronize before returning (device pointers only) */
+  OE_NT_STORES = 4u  /* non-temporal trajectory stores */
+};
+
+/* RNG modes for oe_mh_run */
+enum {
+  OE_RNG_REPLAY = 0, /* caller supplies the proposal increments and uniforms */
+  OE_RNG_PHILOX = 1  /* counter-based Philox4x32-10 keyed by (seed, global walker id) */
+};
+
+typedef struct oe_ctx oe_ctx;
+
+/* The fit problem: everything ModelFramework.__init__ derives from the data. */
+typedef struct {
+  int32_t model_id;          /* OE_MODEL_* */
+  int32_t n_states;          /* S (for OE_MODEL_CHAIN: N) */
+  int32_t n_params;          /* P >= model's own parameter count; extra entries are
+                                e.g. '<state>0' initial-condition parameters */
+  int32_t n_times;           /* T >= 2 */
+  const double* times;       /* [T] host, strictly increasing (np.linspace grid) */
+  int32_t n_obs;             /* number of observations (0 = no likelihood) */
+  const int32_t* obs_tidx;   /* [n_obs] host: grid index (first-nearest, Framework.py:316) */
+  const uint64_t* obs_mask;  /* [n_obs] host: bitmask of ODE states summed into the
+                                observed column (Framework.py:659-664), S <= 64 */
+  const double* obs_log;     /* [n_obs] host: observed log abundance O */
+  const double* obs_logsigma;/* [n_obs] host: log sigma S */
+  const double* obs_lin;     /* [n_obs] host: exp(O) as numpy computes it (Framework.py:700) */
+  int32_t method;            /* OE_METHOD_* */
+  int32_t rk4_substeps;      /* >= 1 */
+  double rtol, atol;         /* DOPRI5 tolerances (odeint defaults 1.49012e-8) */
+  int32_t max_steps;         /* DOPRI5 steps per output interval (odeint mxstep 500) */
+  double sstot;              /* Σ n_s·var(O_s) for R² (stats.py:49-56) */
+  int32_t pnum;              /* parameter count used by AIC (Framework.py:261-263) */
+} oe_problem;
+
+/* Metropolis–Hastings over W independent chains (Samplers.py:53-174). */
+typedef struct {
+  int64_t n_walkers;          /* W (walkers on this device) */
+  int64_t walker_offset;      /* global id of walker 0 (Philox key; sharding across ranks) */
+  int32_t nits;               /* reference nits: iterations 1..nits-1 are run (Samplers.py:84) */
+  int32_t burnin;             /* samples kept for it > burnin (Samplers.py:147) */
+  int32_t rng_mode;           /* OE_RNG_* */
+  int32_t chunk;              /* iterations per kernel launch (0 = library default) */
+  uint64_t seed;              /* Philox seed */
+  double step_sd;             /* log-normal walk sd (Framework.py:107: 0.05) */
+  const uint8_t* walk_mask;   /* [P] host: 1 = parameter walks, 0 = static */
+  const int32_t* init_param;  /* [S] host: -1, or p for a '<state>0' parameter
+                                 (Samplers.py:110-114, :139-143) */
+  const double* replay_dz;    /* [nits-1][P][W] proposal increments (REPLAY) */
+  const double* replay_u;     /* [nits-1][W] acceptance uniforms (REPLAY) */
+  double* theta;              /* [P][W] in: initial θ; out: final θ */
+  double* y0;                 /* [S][W] in: initial states; out: final states */
+  double* samples;            /* [nits-1-burnin][P+5][W] out: θ, chi, rsquared, aic,
+                                 iteration, acceptance_ratio (Samplers.py:160-165) */
+  double* final_stats;        /* [4][W] out (may be NULL): chi, rsquared, aic, n_accepted */
+  int32_t* status;            /* [W] out (may be NULL): status bits of the integration of the
+                                 chain's current (last accepted / initial) state */
+} oe_mh_args;
+
+int oe_abi_version(void);
+
+/* Model registry query: fills S (for CHAIN pass the wanted N in *n_states) and the
+ * model's own parameter count.  Returns OE_ERR_UNSUPPORTED if not compiled in. */
+int oe_model_info(int32_t model_id, int32_t* n_states, int32_t* n_params);
+
+int oe_ctx_create(int32_t device, oe_ctx** out);
+void oe_ctx_destroy(oe_ctx* ctx);
+const char* oe_last_error(const oe_ctx* ctx);
+/* Launch on an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream),
+ * used as given: NULL is the null (legacy default) stream. */
+int oe_ctx_set_stream(oe_ctx* ctx, void* hip_stream);
+/* Launch on the context's own non-blocking stream (the default after oe_ctx_create). */
+int oe_ctx_use_own_stream(oe_ctx* ctx);
+
+int oe_problem_set(oe_ctx* ctx, const oe_problem* problem);
+
+/* Batched integrate + fused likelihood.
+ *   y0     [S][W]    initial states            (Framework.py:647-650)
+ *   theta  [P][W]    parameters                (Framework.py:651-654)
+ *   traj   [T][S][W] full trajectory, or NULL  (the odeint [T,S] output, :656)
+ *   chi    [W] or NULL   Σ_finite (O − log C)²/(2S²)   (stats.py:41), NaN if all masked
+ *   ssres  [W] or NULL   Σ_nan-skipping (C − exp O)²     (stats.py:52)
+ *   status [W] or NULL */
+int oe_integrate(oe_ctx* ctx, int64_t n_walkers, const double* y0, const double* theta,
+                 double* traj, double* chi, double* ssres, int32_t* status, uint32_t flags);
+
+/* Batched Metropolis–Hastings; device pointers only. */
+int oe_mh_run(oe_ctx* ctx, const oe_mh_args* args, uint32_t flags);
+
+/* Device time (ms) of the kernel launches of the last oe_integrate / oe_mh_run,
+ * from HIP events recorded on the context's stream around them (waits for them). */
+int oe_last_kernel_ms(oe_ctx* ctx, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ODELIB_AMD_H */

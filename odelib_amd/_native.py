@@ -1,0 +1,203 @@
+"""ctypes binding of libodelib_amd.so (include/odelib_amd.h).
+
+This is the whole host↔device boundary: plain C pointers and sizes.  The library is
+built in-tree (``odelib_amd/csrc/libodelib_amd.so``, see ``__graft_entry__.build``).
+There is no CPU fallback anywhere in the package: if the library is missing or no
+HIP device is visible, every compute entry point raises ``NativeUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ODELIB_AMD_LIB", os.path.join(_HERE, "csrc", "libodelib_amd.so"))
+
+# --- constants mirrored from include/odelib_amd.h -----------------------------------
+OE_ABI_VERSION = 1
+OE_OK = 0
+OE_METHOD_RK4, OE_METHOD_DOPRI5 = 0, 1
+OE_MODEL_ZERO_I, OE_MODEL_ONE_I, OE_MODEL_TWO_I, OE_MODEL_CHAIN = 0, 1, 2, 3
+OE_STATUS_NONFINITE, OE_STATUS_NEGATIVE, OE_STATUS_MAXSTEP = 1, 2, 4
+OE_HOST_PTRS, OE_ASYNC, OE_NT_STORES = 1, 2, 4
+OE_RNG_REPLAY, OE_RNG_PHILOX = 0, 1
+
+# every symbol include/odelib_amd.h declares (checked by tests/test_abi.py)
+EXPORTED = (
+    "oe_abi_version",
+    "oe_model_info",
+    "oe_ctx_create",
+    "oe_ctx_destroy",
+    "oe_last_error",
+    "oe_ctx_set_stream",
+    "oe_ctx_use_own_stream",
+    "oe_problem_set",
+    "oe_integrate",
+    "oe_mh_run",
+    "oe_last_kernel_ms",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    """The HIP library or a HIP device is missing.  Raised instead of falling back."""
+
+
+class OEProblem(C.Structure):
+    _fields_ = [
+        ("model_id", C.c_int32),
+        ("n_states", C.c_int32),
+        ("n_params", C.c_int32),
+        ("n_times", C.c_int32),
+        ("times", C.c_void_p),
+        ("n_obs", C.c_int32),
+        ("obs_tidx", C.c_void_p),
+        ("obs_mask", C.c_void_p),
+        ("obs_log", C.c_void_p),
+        ("obs_logsigma", C.c_void_p),
+        ("obs_lin", C.c_void_p),
+        ("method", C.c_int32),
+        ("rk4_substeps", C.c_int32),
+        ("rtol", C.c_double),
+        ("atol", C.c_double),
+        ("max_steps", C.c_int32),
+        ("sstot", C.c_double),
+        ("pnum", C.c_int32),
+    ]
+
+
+class OEMHArgs(C.Structure):
+    _fields_ = [
+        ("n_walkers", C.c_int64),
+        ("walker_offset", C.c_int64),
+        ("nits", C.c_int32),
+        ("burnin", C.c_int32),
+        ("rng_mode", C.c_int32),
+        ("chunk", C.c_int32),
+        ("seed", C.c_uint64),
+        ("step_sd", C.c_double),
+        ("walk_mask", C.c_void_p),
+        ("init_param", C.c_void_p),
+        ("replay_dz", C.c_void_p),
+        ("replay_u", C.c_void_p),
+        ("theta", C.c_void_p),
+        ("y0", C.c_void_p),
+        ("samples", C.c_void_p),
+        ("final_stats", C.c_void_p),
+        ("status", C.c_void_p),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str | None = None):
+    """Load (once) and type the shared library.  Importing torch first makes the
+    library bind to the same libamdhip64 instance as PyTorch (same SONAME), so
+    torch device pointers are valid in it."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise NativeUnavailable(
+                f"libodelib_amd.so not found at {p}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C odelib_amd/csrc`")
+        try:
+            import torch  # noqa: F401  (share the HIP runtime with torch)
+        except Exception:  # pragma: no cover - torch is part of the image
+            pass
+        lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+        vp, i32, i64, u32 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32
+        lib.oe_abi_version.restype = C.c_int
+        lib.oe_abi_version.argtypes = []
+        lib.oe_model_info.restype = C.c_int
+        lib.oe_model_info.argtypes = [i32, C.POINTER(i32), C.POINTER(i32)]
+        lib.oe_ctx_create.restype = C.c_int
+        lib.oe_ctx_create.argtypes = [i32, C.POINTER(vp)]
+        lib.oe_ctx_destroy.restype = None
+        lib.oe_ctx_destroy.argtypes = [vp]
+        lib.oe_last_error.restype = C.c_char_p
+        lib.oe_last_error.argtypes = [vp]
+        lib.oe_ctx_set_stream.restype = C.c_int
+        lib.oe_ctx_set_stream.argtypes = [vp, vp]
+        lib.oe_ctx_use_own_stream.restype = C.c_int
+        lib.oe_ctx_use_own_stream.argtypes = [vp]
+        lib.oe_problem_set.restype = C.c_int
+        lib.oe_problem_set.argtypes = [vp, C.POINTER(OEProblem)]
+        lib.oe_integrate.restype = C.c_int
+        lib.oe_integrate.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, u32]
+        lib.oe_mh_run.restype = C.c_int
+        lib.oe_mh_run.argtypes = [vp, C.POINTER(OEMHArgs), u32]
+        lib.oe_last_kernel_ms.restype = C.c_int
+        lib.oe_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+        if lib.oe_abi_version() != OE_ABI_VERSION:
+            raise NativeUnavailable("libodelib_amd.so ABI version mismatch; rebuild it")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def model_info(model_id: int, n_states: int = 0) -> tuple[int, int]:
+    lib = load_library()
+    s, p = C.c_int32(n_states), C.c_int32(0)
+    rc = lib.oe_model_info(model_id, C.byref(s), C.byref(p))
+    if rc != OE_OK:
+        raise ValueError(f"model {model_id} with S={n_states} is not compiled into libodelib_amd.so")
+    return s.value, p.value
+
+
+class Context:
+    """One oe_ctx (device, stream, events, device copy of the problem)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.oe_ctx_create(int(device), C.byref(h))
+        self._h = h
+        if rc != OE_OK:
+            msg = self.lib.oe_last_error(h).decode() if h.value else f"error {rc}"
+            if h.value:
+                self.lib.oe_ctx_destroy(h)
+            self._h = C.c_void_p()
+            raise NativeUnavailable(f"oe_ctx_create({device}) failed: {msg}")
+        self.device = device
+
+    def _check(self, rc: int, what: str):
+        if rc != OE_OK:
+            raise RuntimeError(f"{what} failed ({rc}): {self.lib.oe_last_error(self._h).decode()}")
+
+    def set_stream(self, stream_handle: int):
+        """Launch on this hipStream_t handle (0 = the null stream)."""
+        self._check(self.lib.oe_ctx_set_stream(self._h, C.c_void_p(int(stream_handle))), "oe_ctx_set_stream")
+
+    def use_own_stream(self):
+        self._check(self.lib.oe_ctx_use_own_stream(self._h), "oe_ctx_use_own_stream")
+
+    def problem_set(self, prob: OEProblem):
+        self._check(self.lib.oe_problem_set(self._h, C.byref(prob)), "oe_problem_set")
+
+    def integrate(self, n_walkers, y0, theta, traj, chi, ssres, status, flags=0):
+        self._check(self.lib.oe_integrate(self._h, int(n_walkers), y0, theta, traj, chi, ssres, status,
+                                          int(flags)), "oe_integrate")
+
+    def mh_run(self, args: OEMHArgs, flags=0):
+        self._check(self.lib.oe_mh_run(self._h, C.byref(args), int(flags)), "oe_mh_run")
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_double(0.0)
+        self._check(self.lib.oe_last_kernel_ms(self._h, C.byref(ms)), "oe_last_kernel_ms")
+        return ms.value
+
+    def close(self):
+        if self._h and self._h.value:
+            self.lib.oe_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,427 @@
+// capi.hip — extern "C" implementation of include/odelib_amd.h.
+//
+// Host-side runtime of the engine: context (device, stream, events, scratch),
+// the device copy of the fit problem, the (model, S) → kernel dispatch table,
+// and the chunked Metropolis–Hastings driver.  Nothing here computes on the CPU:
+// every number the API returns was produced by a kernel in ode_kernels.cuh.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/odelib_amd.h"
+#include "dispatch.h"
+
+OE_DECLARE_ENTRY(zero_i);
+OE_DECLARE_ENTRY(one_i);
+OE_DECLARE_ENTRY(two_i);
+OE_DECLARE_ENTRY(chain4);
+OE_DECLARE_ENTRY(chain5);
+OE_DECLARE_ENTRY(chain6);
+OE_DECLARE_ENTRY(chain8);
+OE_DECLARE_ENTRY(chain10);
+OE_DECLARE_ENTRY(chain12);
+OE_DECLARE_ENTRY(chain16);
+OE_DECLARE_ENTRY(chain20);
+OE_DECLARE_ENTRY(chain24);
+OE_DECLARE_ENTRY(chain32);
+
+namespace {
+
+using namespace oe;
+
+const std::vector<Entry>& registry() {
+  static const std::vector<Entry> r = {
+      oe_entry_zero_i(), oe_entry_one_i(),  oe_entry_two_i(),  oe_entry_chain4(),
+      oe_entry_chain5(), oe_entry_chain6(), oe_entry_chain8(), oe_entry_chain10(),
+      oe_entry_chain12(), oe_entry_chain16(), oe_entry_chain20(), oe_entry_chain24(),
+      oe_entry_chain32(),
+  };
+  return r;
+}
+
+const Entry* find_entry(int32_t model_id, int32_t S) {
+  for (const Entry& e : registry()) {
+    if (e.model_id != model_id) continue;
+    if (model_id == OE_MODEL_CHAIN && e.S != S) continue;
+    if (model_id != OE_MODEL_CHAIN && S != 0 && e.S != S) return nullptr;
+    return &e;
+  }
+  return nullptr;
+}
+
+constexpr int kBlock = 256;
+
+}  // namespace
+
+struct oe_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  std::string err;
+  // problem
+  bool has_problem = false;
+  const Entry* entry = nullptr;
+  DevProblem dp{};
+  int32_t method = 0;
+  double* d_times = nullptr;
+  double* d_rk4 = nullptr;
+  Obs* d_obs = nullptr;
+  // scratch
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+};
+
+namespace {
+
+int fail(oe_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define OE_HIP(ctx, expr)                                                              \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(ctx, OE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+int ensure_scratch(oe_ctx* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return OE_OK;
+  if (c->scratch) {
+    OE_HIP(c, hipStreamSynchronize(c->stream));
+    OE_HIP(c, hipFree(c->scratch));
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+  }
+  OE_HIP(c, hipMalloc(&c->scratch, bytes));
+  c->scratch_bytes = bytes;
+  return OE_OK;
+}
+
+int set_device(oe_ctx* c) {
+  OE_HIP(c, hipSetDevice(c->device));
+  return OE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oe_abi_version(void) { return OE_ABI_VERSION; }
+
+int oe_model_info(int32_t model_id, int32_t* n_states, int32_t* n_params) {
+  if (!n_states || !n_params) return OE_ERR_ARG;
+  const Entry* e = find_entry(model_id, *n_states);
+  if (!e) return OE_ERR_UNSUPPORTED;
+  *n_states = e->S;
+  *n_params = e->P;
+  return OE_OK;
+}
+
+int oe_ctx_create(int32_t device, oe_ctx** out) {
+  if (!out) return OE_ERR_ARG;
+  *out = nullptr;
+  oe_ctx* c = new (std::nothrow) oe_ctx();
+  if (!c) return OE_ERR_NOMEM;
+  c->device = device;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || device < 0 || device >= n) {
+    // keep the context so the caller can read the message
+    c->err = std::string("oe_ctx_create: no HIP device ") + std::to_string(device) +
+             " (hipGetDeviceCount=" + std::to_string(n) + ", " + hipGetErrorString(e) + ")";
+    *out = c;
+    return OE_ERR_HIP;
+  }
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    c->err = "oe_ctx_create: HIP initialisation failed";
+    *out = c;
+    return OE_ERR_HIP;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return OE_OK;
+}
+
+void oe_ctx_destroy(oe_ctx* c) {
+  if (!c) return;
+  if (c->own_stream) {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->d_times) (void)hipFree(c->d_times);
+    if (c->d_obs) (void)hipFree(c->d_obs);
+    if (c->d_rk4) (void)hipFree(c->d_rk4);
+    if (c->scratch) (void)hipFree(c->scratch);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    (void)hipStreamDestroy(c->own_stream);
+  }
+  delete c;
+}
+
+const char* oe_last_error(const oe_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int oe_ctx_set_stream(oe_ctx* c, void* s) {
+  if (!c || !c->own_stream) return OE_ERR_STATE;
+  c->stream = static_cast<hipStream_t>(s);  // NULL = the null (legacy default) stream
+  return OE_OK;
+}
+
+int oe_ctx_use_own_stream(oe_ctx* c) {
+  if (!c || !c->own_stream) return OE_ERR_STATE;
+  c->stream = c->own_stream;
+  return OE_OK;
+}
+
+int oe_problem_set(oe_ctx* c, const oe_problem* p) {
+  if (!c || !c->own_stream) return OE_ERR_STATE;
+  if (!p) return fail(c, OE_ERR_ARG, "oe_problem_set: null problem");
+  int rc = set_device(c);
+  if (rc) return rc;
+  const Entry* e = find_entry(p->model_id, p->n_states);
+  if (!e)
+    return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: model " + std::to_string(p->model_id) +
+                                           " with S=" + std::to_string(p->n_states) +
+                                           " is not compiled in");
+  if (p->n_states != e->S) return fail(c, OE_ERR_ARG, "oe_problem_set: n_states mismatch");
+  if (p->n_params < e->P || p->n_params > e->P + e->S || p->n_params > 64)
+    return fail(c, OE_ERR_ARG, "oe_problem_set: n_params must be in [model P, model P + S]");
+  if (p->n_times < 2 || !p->times) return fail(c, OE_ERR_ARG, "oe_problem_set: need >= 2 times");
+  for (int i = 1; i < p->n_times; ++i)
+    if (!(p->times[i] > p->times[i - 1]))
+      return fail(c, OE_ERR_ARG, "oe_problem_set: times must be strictly increasing");
+  if (p->method != OE_METHOD_RK4 && p->method != OE_METHOD_DOPRI5)
+    return fail(c, OE_ERR_ARG, "oe_problem_set: unknown method");
+  if (p->method == OE_METHOD_RK4 && p->rk4_substeps < 1)
+    return fail(c, OE_ERR_ARG, "oe_problem_set: rk4_substeps must be >= 1");
+  if (p->method == OE_METHOD_DOPRI5 &&
+      (!(p->rtol > 0.0) || !(p->atol >= 0.0) || p->max_steps < 2))
+    return fail(c, OE_ERR_ARG, "oe_problem_set: DOPRI5 needs rtol > 0, atol >= 0, max_steps >= 2");
+  if (p->n_obs < 0) return fail(c, OE_ERR_ARG, "oe_problem_set: n_obs < 0");
+  if (p->n_obs > 0 && (!p->obs_tidx || !p->obs_mask || !p->obs_log || !p->obs_logsigma || !p->obs_lin))
+    return fail(c, OE_ERR_ARG, "oe_problem_set: observation arrays missing");
+
+  std::vector<Obs> obs(p->n_obs);
+  const uint64_t valid_mask = (e->S >= 64) ? ~0ull : ((1ull << e->S) - 1ull);
+  for (int k = 0; k < p->n_obs; ++k) {
+    if (p->obs_tidx[k] < 0 || p->obs_tidx[k] >= p->n_times)
+      return fail(c, OE_ERR_ARG, "oe_problem_set: obs_tidx out of range");
+    if (p->obs_mask[k] == 0 || (p->obs_mask[k] & ~valid_mask))
+      return fail(c, OE_ERR_ARG, "oe_problem_set: obs_mask selects no / unknown states");
+    Obs& o = obs[k];
+    o.tidx = p->obs_tidx[k];
+    o.pad = 0;
+    o.mask = p->obs_mask[k];
+    o.O = p->obs_log[k];
+    const double s = p->obs_logsigma[k];
+    o.two_s2 = 2.0 * (s * s);
+    o.O_lin = p->obs_lin[k];
+  }
+  std::stable_sort(obs.begin(), obs.end(), [](const Obs& a, const Obs& b) { return a.tidx < b.tidx; });
+
+  // RK4 per-interval constants: h = (t_i - t_{i-1}) / n, h/2, h/6, t_{i-1}
+  // (IEEE-correctly-rounded on host and device alike, so the table is exact)
+  const int nsub = p->method == OE_METHOD_RK4 ? p->rk4_substeps : 1;
+  std::vector<double> rk4(4 * (size_t)(p->n_times - 1));
+  for (int i = 1; i < p->n_times; ++i) {
+    const double h = (p->times[i] - p->times[i - 1]) / (double)nsub;
+    rk4[4 * (i - 1)] = h;
+    rk4[4 * (i - 1) + 1] = 0.5 * h;
+    rk4[4 * (i - 1) + 2] = h / 6.0;
+    rk4[4 * (i - 1) + 3] = p->times[i - 1];
+  }
+
+  // (re)upload
+  OE_HIP(c, hipStreamSynchronize(c->stream));
+  if (c->d_times) { OE_HIP(c, hipFree(c->d_times)); c->d_times = nullptr; }
+  if (c->d_obs) { OE_HIP(c, hipFree(c->d_obs)); c->d_obs = nullptr; }
+  if (c->d_rk4) { OE_HIP(c, hipFree(c->d_rk4)); c->d_rk4 = nullptr; }
+  OE_HIP(c, hipMalloc(&c->d_rk4, sizeof(double) * rk4.size()));
+  OE_HIP(c, hipMemcpy(c->d_rk4, rk4.data(), sizeof(double) * rk4.size(), hipMemcpyHostToDevice));
+  OE_HIP(c, hipMalloc(&c->d_times, sizeof(double) * p->n_times));
+  OE_HIP(c, hipMemcpy(c->d_times, p->times, sizeof(double) * p->n_times, hipMemcpyHostToDevice));
+  if (p->n_obs > 0) {
+    OE_HIP(c, hipMalloc(&c->d_obs, sizeof(Obs) * p->n_obs));
+    OE_HIP(c, hipMemcpy(c->d_obs, obs.data(), sizeof(Obs) * p->n_obs, hipMemcpyHostToDevice));
+  }
+  DevProblem& d = c->dp;
+  d.times = c->d_times;
+  d.rk4 = c->d_rk4;
+  d.obs = c->d_obs;
+  d.T = p->n_times;
+  d.n_obs = p->n_obs;
+  d.P = p->n_params;
+  d.substeps = p->method == OE_METHOD_RK4 ? p->rk4_substeps : 1;
+  d.rtol = p->rtol;
+  d.atol = p->atol;
+  d.max_steps = p->max_steps;
+  d.pnum = p->pnum;
+  d.sstot = p->sstot;
+  c->method = p->method;
+  c->entry = e;
+  c->has_problem = true;
+  c->err.clear();
+  return OE_OK;
+}
+
+int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, double* traj,
+                 double* chi, double* ssres, int32_t* status, uint32_t flags) {
+  if (!c || !c->own_stream) return OE_ERR_STATE;
+  if (!c->has_problem) return fail(c, OE_ERR_STATE, "oe_integrate: call oe_problem_set first");
+  if (W <= 0) return fail(c, OE_ERR_ARG, "oe_integrate: n_walkers must be > 0");
+  if (!y0 || !theta) return fail(c, OE_ERR_ARG, "oe_integrate: y0 and theta are required");
+  int rc = set_device(c);
+  if (rc) return rc;
+  const Entry* e = c->entry;
+  const int S = e->S, P = c->dp.P, T = c->dp.T;
+  const bool host = flags & OE_HOST_PTRS;
+  const bool nt = flags & OE_NT_STORES;
+
+  IntegrateArgs ia{};
+  ia.W = W;
+  const double* h_y0 = y0;
+  const double* h_th = theta;
+  double* h_traj = traj;
+  double *h_chi = chi, *h_ss = ssres;
+  int32_t* h_st = status;
+  if (host) {
+    const size_t n_in = (size_t)(S + P) * W;
+    const size_t n_traj = traj ? (size_t)T * S * W : 0;
+    const size_t n_out = (size_t)2 * W;
+    const size_t bytes = sizeof(double) * (n_in + n_traj + n_out) + sizeof(int32_t) * W + 256;
+    rc = ensure_scratch(c, bytes);
+    if (rc) return rc;
+    double* base = static_cast<double*>(c->scratch);
+    double* d_y0 = base;
+    double* d_th = d_y0 + (size_t)S * W;
+    double* d_traj = traj ? d_th + (size_t)P * W : nullptr;
+    double* d_chi = d_th + (size_t)P * W + n_traj;
+    double* d_ss = d_chi + W;
+    int32_t* d_st = reinterpret_cast<int32_t*>(d_ss + W);
+    OE_HIP(c, hipMemcpyAsync(d_y0, h_y0, sizeof(double) * S * W, hipMemcpyHostToDevice, c->stream));
+    OE_HIP(c, hipMemcpyAsync(d_th, h_th, sizeof(double) * P * W, hipMemcpyHostToDevice, c->stream));
+    ia.y0 = d_y0; ia.theta = d_th; ia.traj = d_traj; ia.chi = d_chi; ia.ssres = d_ss; ia.status = d_st;
+  } else {
+    ia.y0 = y0; ia.theta = theta; ia.traj = traj; ia.chi = chi; ia.ssres = ssres; ia.status = status;
+  }
+
+  const dim3 grid((unsigned)((W + kBlock - 1) / kBlock)), block(kBlock);
+  OE_HIP(c, hipEventRecord(c->ev0, c->stream));
+  e->integrate[c->method][ia.traj ? 1 : 0][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
+  OE_HIP(c, hipGetLastError());
+  OE_HIP(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+
+  if (host) {
+    if (h_traj)
+      OE_HIP(c, hipMemcpyAsync(h_traj, ia.traj, sizeof(double) * T * S * W, hipMemcpyDeviceToHost, c->stream));
+    if (h_chi) OE_HIP(c, hipMemcpyAsync(h_chi, ia.chi, sizeof(double) * W, hipMemcpyDeviceToHost, c->stream));
+    if (h_ss) OE_HIP(c, hipMemcpyAsync(h_ss, ia.ssres, sizeof(double) * W, hipMemcpyDeviceToHost, c->stream));
+    if (h_st) OE_HIP(c, hipMemcpyAsync(h_st, ia.status, sizeof(int32_t) * W, hipMemcpyDeviceToHost, c->stream));
+    OE_HIP(c, hipStreamSynchronize(c->stream));
+  } else if (!(flags & OE_ASYNC)) {
+    OE_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  return OE_OK;
+}
+
+int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
+  if (!c || !c->own_stream) return OE_ERR_STATE;
+  if (!c->has_problem) return fail(c, OE_ERR_STATE, "oe_mh_run: call oe_problem_set first");
+  if (!a) return fail(c, OE_ERR_ARG, "oe_mh_run: null args");
+  if (flags & OE_HOST_PTRS) return fail(c, OE_ERR_ARG, "oe_mh_run: device pointers only");
+  const Entry* e = c->entry;
+  const int S = e->S, P = c->dp.P;
+  const int64_t W = a->n_walkers;
+  if (W <= 0) return fail(c, OE_ERR_ARG, "oe_mh_run: n_walkers must be > 0");
+  if (a->nits < 1) return fail(c, OE_ERR_ARG, "oe_mh_run: nits must be >= 1");
+  if (a->burnin < 0) return fail(c, OE_ERR_ARG, "oe_mh_run: burnin must be >= 0");
+  if (!a->theta || !a->y0 || !a->walk_mask || !a->init_param)
+    return fail(c, OE_ERR_ARG, "oe_mh_run: theta, y0, walk_mask and init_param are required");
+  const int kept = std::max(0, a->nits - 1 - a->burnin);
+  if (kept > 0 && !a->samples) return fail(c, OE_ERR_ARG, "oe_mh_run: samples buffer required");
+  if (a->rng_mode == OE_RNG_REPLAY) {
+    if (a->nits > 1 && (!a->replay_dz || !a->replay_u))
+      return fail(c, OE_ERR_ARG, "oe_mh_run: replay mode needs replay_dz and replay_u");
+  } else if (a->rng_mode != OE_RNG_PHILOX) {
+    return fail(c, OE_ERR_ARG, "oe_mh_run: unknown rng_mode");
+  }
+  if (S > 64) return fail(c, OE_ERR_UNSUPPORTED, "oe_mh_run: S > 64");
+  int rc = set_device(c);
+  if (rc) return rc;
+
+  MHArgs m{};
+  m.W = W;
+  m.walker_offset = a->walker_offset;
+  m.burnin = a->burnin;
+  m.rng_mode = a->rng_mode;
+  m.seed_lo = (uint32_t)a->seed;
+  m.seed_hi = (uint32_t)(a->seed >> 32);
+  m.step_sd = a->step_sd;
+  m.walk_mask = 0;
+  for (int p = 0; p < P; ++p)
+    if (a->walk_mask[p]) m.walk_mask |= (1ull << p);
+  m.any_walk = m.walk_mask != 0;
+  for (int s = 0; s < 64; ++s) m.init_param[s] = -1;
+  for (int s = 0; s < S; ++s) {
+    const int32_t ip = a->init_param[s];
+    if (ip < -1 || ip >= P) return fail(c, OE_ERR_ARG, "oe_mh_run: init_param out of range");
+    m.init_param[s] = ip;
+  }
+  m.replay_dz = a->replay_dz;
+  m.replay_u = a->replay_u;
+  m.theta = a->theta;
+  m.y0 = a->y0;
+  m.samples = a->samples;
+  m.status = a->status;
+  // chain state: caller's final_stats buffer if given, else scratch
+  if (a->final_stats) {
+    m.cur = a->final_stats;
+  } else {
+    rc = ensure_scratch(c, sizeof(double) * 4 * W);
+    if (rc) return rc;
+    m.cur = static_cast<double*>(c->scratch);
+  }
+
+  const dim3 grid((unsigned)((W + kBlock - 1) / kBlock)), block(kBlock);
+  const int chunk = a->chunk > 0 ? a->chunk : 25;
+  OE_HIP(c, hipEventRecord(c->ev0, c->stream));
+  m.init = 1;
+  m.it0 = 0;
+  m.it1 = 0;
+  e->mh[c->method](c->dp, m, grid, block, c->stream);
+  OE_HIP(c, hipGetLastError());
+  m.init = 0;
+  for (int it0 = 1; it0 < a->nits; it0 += chunk) {
+    m.it0 = it0;
+    m.it1 = std::min(a->nits, it0 + chunk);
+    e->mh[c->method](c->dp, m, grid, block, c->stream);
+    OE_HIP(c, hipGetLastError());
+  }
+  OE_HIP(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  if (!(flags & OE_ASYNC)) OE_HIP(c, hipStreamSynchronize(c->stream));
+  return OE_OK;
+}
+
+int oe_last_kernel_ms(oe_ctx* c, double* ms) {
+  if (!c || !ms) return OE_ERR_ARG;
+  if (!c->timed) return fail(c, OE_ERR_STATE, "oe_last_kernel_ms: nothing launched yet");
+  OE_HIP(c, hipEventSynchronize(c->ev1));
+  float f = 0.f;
+  OE_HIP(c, hipEventElapsedTime(&f, c->ev0, c->ev1));
+  *ms = (double)f;
+  return OE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,55 @@
+// dispatch.h — (model, method, trajectory, store-policy) → kernel launcher table.
+// Each built-in model is instantiated in its own translation unit (inst_*.hip) so the
+// library builds in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "ode_kernels.cuh"
+
+namespace oe {
+
+// ---- dispatch table ---------------------------------------------------------
+using IntegrateLaunch = void (*)(const DevProblem&, const IntegrateArgs&, dim3, dim3, hipStream_t);
+using MHLaunch = void (*)(const DevProblem&, const MHArgs&, dim3, dim3, hipStream_t);
+
+struct Entry {
+  int32_t model_id;
+  int32_t S;
+  int32_t P;  // the model's own parameter count
+  // [method][traj][nt]
+  IntegrateLaunch integrate[2][2][2];
+  MHLaunch mh[2];
+};
+
+template <class M, int METHOD, bool TRAJ, bool NT>
+void launch_integrate(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_integrate<M, METHOD, TRAJ, NT>), g, b, 0, s, pb, ia);
+}
+template <class M, int METHOD>
+void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_mh<M, METHOD>), g, b, 0, s, pb, ma);
+}
+
+template <class M>
+Entry make_entry(int32_t model_id) {
+  Entry e{};
+  e.model_id = model_id;
+  e.S = M::S;
+  e.P = M::P;
+  e.integrate[0][0][0] = launch_integrate<M, 0, false, false>;
+  e.integrate[0][1][0] = launch_integrate<M, 0, true, false>;
+  e.integrate[0][1][1] = launch_integrate<M, 0, true, true>;
+  e.integrate[0][0][1] = launch_integrate<M, 0, false, false>;
+  e.integrate[1][0][0] = launch_integrate<M, 1, false, false>;
+  e.integrate[1][1][0] = launch_integrate<M, 1, true, false>;
+  e.integrate[1][1][1] = launch_integrate<M, 1, true, true>;
+  e.integrate[1][0][1] = launch_integrate<M, 1, false, false>;
+  e.mh[0] = launch_mh<M, 0>;
+  e.mh[1] = launch_mh<M, 1>;
+  return e;
+}
+
+
+}  // namespace oe
+
+// one factory per instantiation unit
+#define OE_DECLARE_ENTRY(NAME) oe::Entry oe_entry_##NAME()

@@ -1,0 +1,596 @@
+// ode_kernels.cuh — batched ODE integration + fused likelihood + Metropolis–Hastings
+// for MI355X (gfx950).  Header-only templates over a Model (models.cuh).
+//
+// Execution model:
+//   * one lane = one walker; state y[S], parameters θ[P] and RK stages live in VGPRs;
+//   * batched HBM layouts are walker-minor: y0/θ are [S|P][W], the trajectory is
+//     [T][S][W], so each wave-instruction moves 64 × 8 B = 512 contiguous bytes;
+//   * the time grid and the observation records are wave-uniform and are read
+//     with scalar loads (SGPR/K$), never per lane;
+//   * the likelihood (get_chi, Framework.py:685-697 / stats.py:41) and the R²
+//     residual (stats.py:52) are accumulated inside the time loop at the
+//     observation grid indices, so MCMC mode writes nothing per time step;
+//   * DOPRI5 runs the 64 lanes of a wavefront in lockstep with one shared step
+//     size: the per-lane max-norm error is max-reduced across the wave with
+//     __shfl_xor, so there is no divergence.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "models.cuh"
+
+namespace oe {
+
+// ---- wave-uniform problem description (device copy made by oe_problem_set) ----
+struct Obs {         // one observation, records sorted by grid index
+  int32_t tidx;      // grid index (Framework.py:316 first-nearest)
+  int32_t pad;
+  uint64_t mask;     // states summed into the observed column (Framework.py:659-664)
+  double O;          // observed log abundance
+  double two_s2;     // 2*(S**2), stats.py:41
+  double O_lin;      // exp(O) as numpy computed it (Framework.py:700)
+};
+
+// Wave-uniform, read-only tables are read through the constant address space so the
+// loads are scalar (s_load → lgkmcnt).  A generic-pointer load would be a vector load
+// the compiler must order against the trajectory stores, i.e. an s_waitcnt vmcnt(0)
+// that drains every outstanding store each time step.
+template <class T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <class T>
+__device__ __forceinline__ cptr<T> kconst(const T* p) {
+  return (cptr<T>)(p);
+}
+
+struct DevProblem {
+  const double* times;  // [T]
+  const double* rk4;    // [T-1][4]: h, h/2, h/6, t_i  (host-computed per interval)
+  const Obs* obs;       // [n_obs]
+  int32_t T;
+  int32_t n_obs;
+  int32_t P;            // runtime parameter count (<= Model::P + Model::S)
+  int32_t substeps;     // RK4 steps per output interval
+  double rtol, atol;
+  int32_t max_steps;    // DOPRI5 steps per output interval
+  int32_t pnum;         // AIC parameter count
+  double sstot;         // R² denominator
+};
+
+enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4 };
+
+// per-lane accumulators of the fused likelihood
+struct Acc {
+  double chi;     // Σ finite (O - log C)^2 / (2 S^2)
+  double ssres;   // Σ non-NaN (C - O_lin)^2
+  double nf;      // Σ y*0 over emitted states: NaN iff some state was non-finite
+  double ymin;    // min over emitted states (fmin ignores NaN)
+  int32_t nvalid; // number of finite chi terms
+  int32_t status; // MAXSTEP bit set by DOPRI5; the other bits come from finish()
+};
+
+__device__ __forceinline__ Acc acc_init() { return Acc{0.0, 0.0, 0.0, __builtin_inf(), 0, 0}; }
+
+__device__ __forceinline__ int32_t finish(const Acc& a) {
+  int32_t st = a.status;
+  if (__builtin_isnan(a.nf)) st |= ST_NONFINITE;
+  if (a.ymin < 0.0) st |= ST_NEGATIVE;
+  return st;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// register-array element at a (uniform) runtime index without spilling the array
+// to scratch: a compile-time-unrolled select chain
+template <int N>
+__device__ __forceinline__ double pick(const double (&a)[N], int idx) {
+  double v = 0.0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) v = (j == idx) ? a[j] : v;
+  return v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void st(double* p, double v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// Emit grid point i: store the trajectory row (TRAJ), flag status, and fold every
+// observation recorded at grid index i into the likelihood.  `k` is the
+// wave-uniform observation cursor.
+template <int S, bool TRAJ, bool NT>
+__device__ __forceinline__ void emit(const DevProblem& pb, int i, const double (&y)[S],
+                                     double* __restrict__ traj, int64_t W, int64_t w,
+                                     bool active, int& k, Acc& a) {
+  if constexpr (TRAJ) {
+    if (active) {
+      double* row = traj + (int64_t)i * S * W + w;
+#pragma unroll
+      for (int s = 0; s < S; ++s) st<NT>(row + (int64_t)s * W, y[s]);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    a.nf = fma(y[s], 0.0, a.nf);
+    a.ymin = fmin(a.ymin, y[s]);
+  }
+  const cptr<Obs> obs = kconst(pb.obs);
+  while (k < pb.n_obs && obs[k].tidx == i) {
+    const uint64_t mask = obs[k].mask;
+    const double O = obs[k].O, two_s2 = obs[k].two_s2, O_lin = obs[k].O_lin;
+    double c = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      if ((mask >> s) & 1ull) c = c + y[s];  // increasing state order, as numpy's sum
+    // chi term, in the operation order of stats.py:41
+    const double d = O - log(c);
+    const double term = (d * d) / two_s2;
+    if (__builtin_isfinite(term)) { a.chi += term; a.nvalid += 1; }
+    // R² residual (stats.py:52 np.nansum skips NaN only)
+    const double r = c - O_lin;
+    const double r2 = r * r;
+    if (!__builtin_isnan(r2)) a.ssres += r2;
+    ++k;
+  }
+}
+
+template <int S, bool TRAJ>
+__device__ __forceinline__ bool grid_needs_emit(const DevProblem& pb, int i, int k) {
+  if constexpr (TRAJ) return true;
+  return k < pb.n_obs && kconst(pb.obs)[k].tidx == i;
+}
+
+// ---------------------------------------------------------------------------------
+// Fixed-step classical RK4; `substeps` steps per output interval.  Operation order
+// (restated independently in oracle/rk_ref.c):
+//   h = (t_i - t_{i-1})/n; hh = 0.5*h; h6 = h/6 (host table); substep j starts at t_{i-1} + j*h
+//   k1 = f(t, y); yt = fma(hh,k1,y); k2 = f(t+hh, yt); yt = fma(hh,k2,y);
+//   k3 = f(t+hh, yt); yt = fma(h,k3,y); k4 = f(t+h, yt)
+//   acc = fma(2,k2,k1); acc = fma(2,k3,acc); acc = acc + k4; y = fma(h6,acc,y)
+// ---------------------------------------------------------------------------------
+template <class M, int PMAX>
+__device__ __forceinline__ void rk4_step(double (&y)[M::S], double t, double h, double hh, double h6,
+                                         const double (&p)[PMAX]) {
+  constexpr int S = M::S;
+  double k[S], acc[S], yt[S];
+  M::rhs(y, t, p, k);
+#pragma unroll
+  for (int s = 0; s < S; ++s) { acc[s] = k[s]; yt[s] = fma(hh, k[s], y[s]); }
+  M::rhs(yt, t + hh, p, k);
+#pragma unroll
+  for (int s = 0; s < S; ++s) { acc[s] = fma(2.0, k[s], acc[s]); yt[s] = fma(hh, k[s], y[s]); }
+  M::rhs(yt, t + hh, p, k);
+#pragma unroll
+  for (int s = 0; s < S; ++s) { acc[s] = fma(2.0, k[s], acc[s]); yt[s] = fma(h, k[s], y[s]); }
+  M::rhs(yt, t + h, p, k);
+#pragma unroll
+  for (int s = 0; s < S; ++s) { acc[s] = acc[s] + k[s]; y[s] = fma(h6, acc[s], y[s]); }
+}
+
+template <class M, int PMAX, bool TRAJ, bool NT>
+__device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[M::S],
+                                              const double (&p)[PMAX], double* traj,
+                                              int64_t W, int64_t w, bool active, Acc& a) {
+  int k = 0;
+  emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, w, active, k, a);
+  const int n = pb.substeps;
+  const cptr<double> tab = kconst(pb.rk4);
+  for (int i = 1; i < pb.T; ++i) {
+    // per-interval constants, computed on the host exactly as written here:
+    // h = (t_i - t_{i-1}) / n, hh = 0.5*h, h6 = h/6
+    const double h = tab[4 * (i - 1)], hh = tab[4 * (i - 1) + 1], h6 = tab[4 * (i - 1) + 2];
+    const double t = tab[4 * (i - 1) + 3];
+    for (int j = 0; j < n; ++j) rk4_step<M, PMAX>(y, t + (double)j * h, h, hh, h6, p);
+    if (grid_needs_emit<M::S, TRAJ>(pb, i, k)) emit<M::S, TRAJ, NT>(pb, i, y, traj, W, w, active, k, a);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Dormand–Prince 5(4) with FSAL and Hairer's 4th-order dense output; the 64 lanes
+// of a wave share one step size (wave max of the per-lane max-norm error
+//   err_lane = max_s |e_s| / (atol + rtol*max(|y_s|, |ynew_s|))).
+// Walkers that pin the wave's step beyond the budget are evicted (status MAXSTEP,
+// NaN output) so the rest of the wave keeps going.
+// ---------------------------------------------------------------------------------
+namespace dp {
+constexpr double c2 = 1.0 / 5, c3 = 3.0 / 10, c4 = 4.0 / 5, c5 = 8.0 / 9;
+constexpr double a21 = 1.0 / 5;
+constexpr double a31 = 3.0 / 40, a32 = 9.0 / 40;
+constexpr double a41 = 44.0 / 45, a42 = -56.0 / 15, a43 = 32.0 / 9;
+constexpr double a51 = 19372.0 / 6561, a52 = -25360.0 / 2187, a53 = 64448.0 / 6561,
+                 a54 = -212.0 / 729;
+constexpr double a61 = 9017.0 / 3168, a62 = -355.0 / 33, a63 = 46732.0 / 5247,
+                 a64 = 49.0 / 176, a65 = -5103.0 / 18656;
+constexpr double a71 = 35.0 / 384, a73 = 500.0 / 1113, a74 = 125.0 / 192,
+                 a75 = -2187.0 / 6784, a76 = 11.0 / 84;
+constexpr double e1 = 71.0 / 57600, e3 = -71.0 / 16695, e4 = 71.0 / 1920,
+                 e5 = -17253.0 / 339200, e6 = 22.0 / 525, e7 = -1.0 / 40;
+constexpr double d1 = -12715105075.0 / 11282082432.0, d3 = 87487479700.0 / 32700410799.0,
+                 d4 = -10690763975.0 / 1880347072.0, d5 = 701980252875.0 / 199316789632.0,
+                 d6 = -1453857185.0 / 822651844.0, d7 = 69997945.0 / 29380423.0;
+constexpr double safe = 0.9, facmin = 0.2, facmax = 10.0;
+}  // namespace dp
+
+template <class M, int PMAX, bool TRAJ, bool NT>
+__device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
+                                                 const double (&p)[PMAX], double* traj,
+                                                 int64_t W, int64_t w, bool active, Acc& a) {
+  using namespace dp;
+  constexpr int S = M::S;
+  int k = 0;
+  emit<S, TRAJ, NT>(pb, 0, y, traj, W, w, active, k, a);
+  const cptr<double> times = kconst(pb.times);
+  const double t0 = times[0];
+  const double tend = times[pb.T - 1];
+  const double rtol = pb.rtol, atol = pb.atol;
+  bool dead = !active;  // dead lanes never enter the wave norm
+  double t = t0;
+  double k1[S], k2[S], k3[S], k4[S], k5[S], k6[S], k7[S], yt[S], yn[S];
+  M::rhs(y, t, p, k1);
+
+  // ---- initial step: Hairer's HINIT per lane (max norm), wave minimum ----
+  double h;
+  {
+    double d0 = 0.0, d1v = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double sk = atol + rtol * fabs(y[s]);
+      d0 = fmax(d0, fabs(y[s]) / sk);
+      d1v = fmax(d1v, fabs(k1[s]) / sk);
+    }
+    double h0 = (d0 <= 1e-5 || d1v <= 1e-5) ? 1e-6 : 0.01 * (d0 / d1v);
+    h0 = fmin(h0, tend - t0);
+#pragma unroll
+    for (int s = 0; s < S; ++s) yt[s] = fma(h0, k1[s], y[s]);
+    M::rhs(yt, t + h0, p, k2);
+    double d2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double sk = atol + rtol * fabs(y[s]);
+      d2 = fmax(d2, fabs(k2[s] - k1[s]) / sk);
+    }
+    d2 = d2 / h0;
+    const double dm = fmax(d1v, d2);
+    const double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / dm, 0.2);
+    double hl = fmin(100.0 * h0, h1);
+    if (dead || !__builtin_isfinite(hl) || !(hl > 0.0)) hl = tend - t0;
+    h = wave_min(hl);
+    h = fmin(h, tend - t0);
+  }
+
+  const double span = tend - t0;
+  const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
+  int i = 1;
+  int nst = 0;  // steps since the last grid point
+  bool last_rej = false;
+  while (i < pb.T) {
+    bool last = false;
+    if (t + h >= tend) { h = tend - t; last = true; }
+    // ---- stages ----
+#pragma unroll
+    for (int s = 0; s < S; ++s) yt[s] = y[s] + h * (a21 * k1[s]);
+    M::rhs(yt, t + c2 * h, p, k2);
+#pragma unroll
+    for (int s = 0; s < S; ++s) yt[s] = y[s] + h * (a31 * k1[s] + a32 * k2[s]);
+    M::rhs(yt, t + c3 * h, p, k3);
+#pragma unroll
+    for (int s = 0; s < S; ++s) yt[s] = y[s] + h * (a41 * k1[s] + a42 * k2[s] + a43 * k3[s]);
+    M::rhs(yt, t + c4 * h, p, k4);
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      yt[s] = y[s] + h * (a51 * k1[s] + a52 * k2[s] + a53 * k3[s] + a54 * k4[s]);
+    M::rhs(yt, t + c5 * h, p, k5);
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      yt[s] = y[s] + h * (a61 * k1[s] + a62 * k2[s] + a63 * k3[s] + a64 * k4[s] + a65 * k5[s]);
+    M::rhs(yt, t + h, p, k6);
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      yn[s] = y[s] + h * (a71 * k1[s] + a73 * k3[s] + a74 * k4[s] + a75 * k5[s] + a76 * k6[s]);
+    M::rhs(yn, t + h, p, k7);
+    // ---- per-lane max-norm error, wave max ----
+    double el = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double e = h * (e1 * k1[s] + e3 * k3[s] + e4 * k4[s] + e5 * k5[s] + e6 * k6[s] + e7 * k7[s]);
+      const double sk = atol + rtol * fmax(fabs(y[s]), fabs(yn[s]));
+      el = fmax(el, fabs(e) / sk);
+    }
+    if (!__builtin_isfinite(el)) el = 1e30;  // also catches NaN (fmax would drop it)
+    if (dead) el = 0.0;
+    const double err = wave_max(el);
+    ++nst;
+
+    if (err <= 1.0) {
+      const double tn = last ? tend : t + h;
+      // dense output for every grid point in (t, tn]
+      while (i < pb.T && times[i] <= tn) {
+        if (grid_needs_emit<S, TRAJ>(pb, i, k)) {
+          double yo[S];
+          const double ti = times[i];
+          if (ti == tn) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) yo[s] = yn[s];
+          } else {
+            const double th = (ti - t) / h;
+            const double th1 = 1.0 - th;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+              const double ydiff = yn[s] - y[s];
+              const double bspl = h * k1[s] - ydiff;
+              const double r4 = ydiff - h * k7[s] - bspl;
+              const double r5 = h * (d1 * k1[s] + d3 * k3[s] + d4 * k4[s] + d5 * k5[s] +
+                                     d6 * k6[s] + d7 * k7[s]);
+              yo[s] = y[s] + th * (ydiff + th1 * (bspl + th * (r4 + th1 * r5)));
+            }
+          }
+          if (dead) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
+          }
+          emit<S, TRAJ, NT>(pb, i, yo, traj, W, w, active, k, a);
+        }
+        ++i;
+        nst = 0;
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) { y[s] = yn[s]; k1[s] = k7[s]; }
+      t = tn;
+      double fac = (err > 0.0) ? safe * pow(err, -0.2) : facmax;
+      fac = fmin(facmax, fmax(facmin, fac));
+      if (last_rej) fac = fmin(fac, 1.0);
+      h = h * fac;
+      last_rej = false;
+    } else {
+      h = h * fmax(facmin, safe * pow(err, -0.2));
+      last_rej = true;
+    }
+    // ---- budget: evict the walkers that pin the wave's step ----
+    if (nst >= pb.max_steps || h < hmin) {
+      if (!dead && el >= 0.5 * err) { dead = true; a.status |= ST_MAXSTEP; }
+      nst = pb.max_steps / 2;
+      const double alive = wave_max(dead ? 0.0 : 1.0);
+      if (alive == 0.0) {
+        // every lane is out: emit NaN rows for the rest of the grid and stop
+        double yo[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
+        for (; i < pb.T; ++i)
+          if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, w, active, k, a);
+        break;
+      }
+      if (h < hmin) h = fmin(1e-3 * span, tend - t);
+    }
+  }
+  if (dead && active) a.status |= ST_MAXSTEP;
+}
+
+template <class M, int PMAX, int METHOD, bool TRAJ, bool NT>
+__device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&y)[M::S],
+                                                 const double (&p)[PMAX], double* traj,
+                                                 int64_t W, int64_t w, bool active, Acc& a) {
+  if constexpr (METHOD == 0) integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, w, active, a);
+  else integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, w, active, a);
+}
+
+// ---------------------------------------------------------------------------------
+// Kernel 1: batched integrate (+ fused chi / R² residual).
+// ---------------------------------------------------------------------------------
+struct IntegrateArgs {
+  int64_t W;
+  const double* y0;     // [S][W]
+  const double* theta;  // [P][W]
+  double* traj;         // [T][S][W] or null
+  double* chi;          // [W] or null
+  double* ssres;        // [W] or null
+  int32_t* status;      // [W] or null
+};
+
+template <class M, int METHOD, bool TRAJ, bool NT>
+__global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const IntegrateArgs ia) {
+  constexpr int S = M::S;
+  constexpr int PMAX = M::P + M::S;
+  const int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = gw < ia.W;
+  const int64_t w = active ? gw : ia.W - 1;  // tail lanes shadow the last walker, never store
+  const int64_t W = ia.W;
+  double y[S], p[PMAX];
+#pragma unroll
+  for (int s = 0; s < S; ++s) y[s] = ia.y0[(int64_t)s * W + w];
+#pragma unroll
+  for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
+  Acc a = acc_init();
+  integrate_walker<M, PMAX, METHOD, TRAJ, NT>(pb, y, p, ia.traj, W, w, active, a);
+  if (active) {
+    if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
+    if (ia.ssres) ia.ssres[w] = a.ssres;
+    if (ia.status) ia.status[w] = finish(a);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11) counter-based RNG for the MH proposals.
+// ---------------------------------------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = U4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
+           (uint32_t)p0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// 53-bit uniform in [0,1) from two words (numpy random_sample construction)
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// ---------------------------------------------------------------------------------
+// Kernel 2: Metropolis–Hastings, iterations [it0, it1) for every walker
+// (Samplers.py:104-153).  One lane = one chain; the chain state lives in HBM
+// between chunked launches.
+// ---------------------------------------------------------------------------------
+struct MHArgs {
+  int64_t W;
+  int64_t walker_offset;
+  int32_t it0, it1;        // iteration range of this launch (1-based, ref `it`)
+  int32_t burnin;
+  int32_t rng_mode;        // 0 replay, 1 philox
+  int32_t init;            // 1: compute the a-priori chi/R²/AIC only (Samplers.py:88-91)
+  int32_t any_walk;
+  uint64_t walk_mask;      // bit p: parameter p walks
+  uint32_t seed_lo, seed_hi;
+  double step_sd;
+  int32_t init_param[64];  // per state: -1 or parameter index
+  const double* replay_dz; // [nits-1][P][W]
+  const double* replay_u;  // [nits-1][W]
+  double* theta;           // [P][W]
+  double* y0;              // [S][W]
+  double* samples;         // [kept][P+5][W]
+  double* cur;             // [4][W]: chi, rsquared, aic, n_accepted
+  int32_t* status;         // [W]
+};
+
+template <class M, int METHOD>
+__global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma) {
+  constexpr int S = M::S;
+  constexpr int PMAX = M::P + M::S;
+  const int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = gw < ma.W;
+  const int64_t w = active ? gw : ma.W - 1;
+  const int64_t W = ma.W;
+  const int P = pb.P;
+  double th[PMAX], y0[S];
+#pragma unroll
+  for (int j = 0; j < PMAX; ++j) th[j] = (j < P) ? ma.theta[(int64_t)j * W + w] : 0.0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) y0[s] = ma.y0[(int64_t)s * W + w];
+
+  if (ma.init) {  // a-priori fit (Samplers.py:88-91)
+    double y[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) y[s] = y0[s];
+    Acc a = acc_init();
+    integrate_walker<M, PMAX, METHOD, false, false>(pb, y, th, nullptr, W, w, active, a);
+    if (active) {
+      const double chi = a.nvalid ? a.chi : __builtin_nan("");
+      ma.cur[w] = chi;
+      ma.cur[W + w] = 1.0 - a.ssres / pb.sstot;
+      ma.cur[2 * W + w] = -2.0 * (-chi) + 2.0 * (double)pb.pnum;
+      ma.cur[3 * W + w] = 0.0;
+      if (ma.status) ma.status[w] = finish(a);
+    }
+    return;
+  }
+
+  double chi = ma.cur[w], rsq = ma.cur[W + w], aic = ma.cur[2 * W + w];
+  double nacc = ma.cur[3 * W + w];
+  int32_t status = ma.status ? ma.status[w] : 0;
+  const uint64_t gid = (uint64_t)(ma.walker_offset + w);
+  const int PS = P + 5;
+
+  for (int it = ma.it0; it < ma.it1; ++it) {
+    // ---- proposal: θ' = exp(log θ + N(0, sd)) for walking parameters (Framework.py:107-122)
+    double tn[PMAX];
+    double u;
+    if (ma.rng_mode == 0) {
+      const double* dz = ma.replay_dz + (int64_t)(it - 1) * P * W + w;
+#pragma unroll
+      for (int j = 0; j < PMAX; ++j)
+        tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? exp(log(th[j]) + dz[(int64_t)j * W]) : th[j];
+      u = ma.replay_u[(int64_t)(it - 1) * W + w];
+    } else {
+      double z[PMAX + 1];
+#pragma unroll
+      for (int j = 0; j < PMAX; j += 2) {
+        const U4 r = philox4x32_10(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, (uint32_t)(j >> 1)},
+                                   ma.seed_lo, ma.seed_hi);
+        const double u1 = 1.0 - u53(r.x, r.y);
+        const double u2 = u53(r.z, r.w);
+        const double rad = sqrt(-2.0 * log(u1));
+        const double ang = 6.283185307179586 * u2;
+        z[j] = rad * cos(ang);
+        z[j + 1] = rad * sin(ang);
+      }
+      const U4 r = philox4x32_10(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, 0x80000000u},
+                                 ma.seed_lo, ma.seed_hi);
+      u = u53(r.x, r.y);
+#pragma unroll
+      for (int j = 0; j < PMAX; ++j)
+        tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? exp(log(th[j]) + ma.step_sd * z[j]) : th[j];
+    }
+    // '<state>0' parameters drive initial states (Samplers.py:110-114)
+    double y[S], yp0[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pi = ma.init_param[s];
+      yp0[s] = (ma.any_walk && pi >= 0) ? pick(tn, pi) : y0[s];
+      y[s] = yp0[s];
+    }
+    // ---- integrate + fused chi (Samplers.py:115-116)
+    Acc a = acc_init();
+    integrate_walker<M, PMAX, METHOD, false, false>(pb, y, tn, nullptr, W, w, active, a);
+    const double chin = a.nvalid ? a.chi : __builtin_nan("");
+    // ---- acceptance, in the reference's arithmetic (Samplers.py:124-127)
+    const double lr = exp(chi - chin);
+    const double accp = exp(log(lr));
+    if (accp > u) {
+      chi = chin;
+      rsq = 1.0 - a.ssres / pb.sstot;
+      aic = -2.0 * (-chi) + 2.0 * (double)pb.pnum;
+#pragma unroll
+      for (int j = 0; j < PMAX; ++j) th[j] = tn[j];
+#pragma unroll
+      for (int s = 0; s < S; ++s) y0[s] = yp0[s];
+      nacc += 1.0;
+      status = finish(a);
+    } else {
+      // reject: parameters restored, linked initial states follow them (Samplers.py:137-143)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pi = ma.init_param[s];
+        if (ma.any_walk && pi >= 0) y0[s] = pick(th, pi);
+      }
+    }
+    // ---- keep the sample after burn-in (Samplers.py:147-153)
+    if (it > ma.burnin && active) {
+      double* row = ma.samples + (int64_t)(it - ma.burnin - 1) * PS * W + w;
+#pragma unroll
+      for (int j = 0; j < PMAX; ++j)
+        if (j < P) row[(int64_t)j * W] = th[j];
+      row[(int64_t)P * W] = chi;
+      row[(int64_t)(P + 1) * W] = rsq;
+      row[(int64_t)(P + 2) * W] = aic;
+      row[(int64_t)(P + 3) * W] = (double)it;
+      row[(int64_t)(P + 4) * W] = nacc / (double)it;
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j)
+      if (j < P) ma.theta[(int64_t)j * W + w] = th[j];
+#pragma unroll
+    for (int s = 0; s < S; ++s) ma.y0[(int64_t)s * W + w] = y0[s];
+    ma.cur[w] = chi;
+    ma.cur[W + w] = rsq;
+    ma.cur[2 * W + w] = aic;
+    ma.cur[3 * W + w] = nacc;
+    if (ma.status) ma.status[w] = status;
+  }
+}
+
+}  // namespace oe

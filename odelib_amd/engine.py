@@ -1,0 +1,235 @@
+"""Batched engine: device-resident walkers over the C-ABI.
+
+``FitProblem`` is the host description of one fit (what ``ModelFramework.__init__``
+derives from the data, ODElib/Framework.py:226-258); ``Engine`` owns an ``oe_ctx``
+with that problem uploaded and runs
+
+* ``integrate``  — W walkers through ``oe_integrate`` (Framework.py:622-697 batched):
+  trajectory ``[T][S][W]``, fused chi / R² residual, status;
+* ``mh_run``     — W independent Metropolis–Hastings chains through ``oe_mh_run``
+  (Statistics/Samplers.py:53-174 batched, one chain per walker).
+
+Tensors are torch tensors on ``cuda:<device>`` (PyTorch provides device memory and the
+stream); the arithmetic happens in the HIP kernels only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as N
+
+METHODS = {"rk4": N.OE_METHOD_RK4, "dopri5": N.OE_METHOD_DOPRI5}
+ODEINT_TOL = 1.49012e-8  # scipy.integrate.odeint default rtol/atol (Framework.py:656)
+
+
+@dataclass
+class FitProblem:
+    """Wave-uniform inputs of the fused integrate+likelihood kernel."""
+    model_id: int
+    n_states: int
+    n_params: int
+    times: np.ndarray                       # [T] float64
+    obs_tidx: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    obs_mask: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint64))
+    obs_log: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    obs_logsigma: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    obs_lin: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    sstot: float = 1.0
+    pnum: int = 0
+    method: str = "rk4"
+    rk4_substeps: int = 1
+    rtol: float = ODEINT_TOL
+    atol: float = ODEINT_TOL
+    max_steps: int = 500
+
+    def __post_init__(self):
+        self.times = np.ascontiguousarray(self.times, dtype=np.float64)
+        self.obs_tidx = np.ascontiguousarray(self.obs_tidx, dtype=np.int32)
+        self.obs_mask = np.ascontiguousarray(self.obs_mask, dtype=np.uint64)
+        self.obs_log = np.ascontiguousarray(self.obs_log, dtype=np.float64)
+        self.obs_logsigma = np.ascontiguousarray(self.obs_logsigma, dtype=np.float64)
+        self.obs_lin = np.ascontiguousarray(self.obs_lin, dtype=np.float64)
+        n = len(self.obs_tidx)
+        for a in (self.obs_mask, self.obs_log, self.obs_logsigma, self.obs_lin):
+            if len(a) != n:
+                raise ValueError("observation arrays must have equal length")
+        if self.method not in METHODS:
+            raise ValueError(f"method must be one of {sorted(METHODS)}")
+
+    @property
+    def n_times(self) -> int:
+        return len(self.times)
+
+    @property
+    def n_obs(self) -> int:
+        return len(self.obs_tidx)
+
+    def to_c(self) -> N.OEProblem:
+        p = N.OEProblem()
+        p.model_id = int(self.model_id)
+        p.n_states = int(self.n_states)
+        p.n_params = int(self.n_params)
+        p.n_times = int(self.n_times)
+        p.times = self.times.ctypes.data
+        p.n_obs = int(self.n_obs)
+        p.obs_tidx = self.obs_tidx.ctypes.data if self.n_obs else None
+        p.obs_mask = self.obs_mask.ctypes.data if self.n_obs else None
+        p.obs_log = self.obs_log.ctypes.data if self.n_obs else None
+        p.obs_logsigma = self.obs_logsigma.ctypes.data if self.n_obs else None
+        p.obs_lin = self.obs_lin.ctypes.data if self.n_obs else None
+        p.method = METHODS[self.method]
+        p.rk4_substeps = int(self.rk4_substeps)
+        p.rtol = float(self.rtol)
+        p.atol = float(self.atol)
+        p.max_steps = int(self.max_steps)
+        p.sstot = float(self.sstot)
+        p.pnum = int(self.pnum)
+        return p
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class Engine:
+    """A device context with one FitProblem uploaded."""
+
+    def __init__(self, problem: FitProblem, device: int = 0, use_torch_stream: bool = True):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise N.NativeUnavailable("no HIP device visible to torch; the engine has no CPU path")
+        self.torch = torch
+        self.device = int(device)
+        self.dev = torch.device("cuda", self.device)
+        self.ctx = N.Context(self.device)
+        self.use_torch_stream = use_torch_stream
+        self.problem = None
+        self.set_problem(problem)
+
+    # -- problem ---------------------------------------------------------------------------
+    def set_problem(self, problem: FitProblem):
+        self._sync_stream()
+        self.ctx.problem_set(problem.to_c())
+        self.problem = problem
+
+    def _sync_stream(self):
+        if self.use_torch_stream:
+            s = self.torch.cuda.current_stream(self.dev)
+            self.ctx.set_stream(s.cuda_stream)
+
+    # -- helpers -----------------------------------------------------------------------------
+    def _dev(self, a, shape, dtype=None):
+        torch = self.torch
+        dtype = dtype or torch.float64
+        if isinstance(a, torch.Tensor):
+            t = a.to(device=self.dev, dtype=dtype)
+        else:
+            t = torch.as_tensor(np.asarray(a), dtype=dtype, device=self.dev)
+        t = t.contiguous()
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"expected shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t
+
+    def empty_traj(self, n_walkers: int):
+        pb = self.problem
+        return self.torch.empty((pb.n_times, pb.n_states, n_walkers), dtype=self.torch.float64, device=self.dev)
+
+    # -- batched integrate -------------------------------------------------------------------
+    def integrate(self, y0, theta, trajectory: bool = True, traj_out=None, nt_stores: bool = True,
+                  sync: bool = True):
+        """y0 [S][W], theta [P][W] → dict(traj [T][S][W] | None, chi [W], ssres [W], status [W])."""
+        torch = self.torch
+        pb = self.problem
+        theta_t = theta if isinstance(theta, torch.Tensor) else np.asarray(theta)
+        W = int(theta_t.shape[1])
+        y0 = self._dev(y0, (pb.n_states, W))
+        theta = self._dev(theta, (pb.n_params, W))
+        traj = None
+        if trajectory:
+            traj = traj_out if traj_out is not None else self.empty_traj(W)
+            if tuple(traj.shape) != (pb.n_times, pb.n_states, W) or traj.dtype != torch.float64 \
+                    or not traj.is_contiguous() or traj.device != self.dev:
+                raise ValueError("traj_out must be a contiguous float64 [T][S][W] tensor on the engine device")
+        chi = torch.empty(W, dtype=torch.float64, device=self.dev)
+        ssres = torch.empty(W, dtype=torch.float64, device=self.dev)
+        status = torch.empty(W, dtype=torch.int32, device=self.dev)
+        self._sync_stream()
+        flags = N.OE_ASYNC | (N.OE_NT_STORES if nt_stores else 0)
+        self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)
+        if sync:
+            torch.cuda.synchronize(self.dev)
+        return {"traj": traj, "chi": chi, "ssres": ssres, "status": status}
+
+    def last_kernel_ms(self) -> float:
+        return self.ctx.last_kernel_ms()
+
+    # -- batched Metropolis–Hastings ---------------------------------------------------------
+    def mh_run(self, theta, y0, nits: int, burnin: int, walk_mask, init_param=None, rng: str = "philox",
+               seed: int = 0, replay=None, step_sd: float = 0.05, walker_offset: int = 0, chunk: int = 0,
+               sync: bool = True):
+        """Run W chains; returns dict(samples [kept][P+5][W], theta, y0, final [4][W], status).
+
+        rng='replay' takes ``replay=(dz [nits-1][P][W], u [nits-1][W])`` (e.g. from
+        ``odelib_amd.rng.legacy_replay_streams``) and reproduces the reference's numpy
+        draws; rng='philox' draws on device, keyed by (seed, walker_offset + w)."""
+        torch = self.torch
+        pb = self.problem
+        P, S = pb.n_params, pb.n_states
+        W = int((theta if isinstance(theta, torch.Tensor) else np.asarray(theta)).shape[1])
+        theta = self._dev(theta, (P, W)).clone()
+        y0 = self._dev(y0, (S, W)).clone()
+        nits = int(nits)
+        burnin = int(burnin)
+        kept = max(0, nits - 1 - burnin)
+        samples = torch.empty((max(kept, 1), P + 5, W), dtype=torch.float64, device=self.dev)
+        final = torch.empty((4, W), dtype=torch.float64, device=self.dev)
+        status = torch.zeros(W, dtype=torch.int32, device=self.dev)
+        wm = np.ascontiguousarray(np.asarray(walk_mask, dtype=np.uint8).reshape(P))
+        ip = np.full(S, -1, np.int32) if init_param is None else np.ascontiguousarray(
+            np.asarray(init_param, dtype=np.int32).reshape(S))
+        a = N.OEMHArgs()
+        a.n_walkers = W
+        a.walker_offset = int(walker_offset)
+        a.nits = nits
+        a.burnin = burnin
+        a.chunk = int(chunk)
+        a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        a.step_sd = float(step_sd)
+        a.walk_mask = wm.ctypes.data
+        a.init_param = ip.ctypes.data
+        keep = []
+        if rng == "replay":
+            if replay is None:
+                raise ValueError("rng='replay' needs replay=(dz, u)")
+            dz = self._dev(replay[0], (max(nits - 1, 0), P, W))
+            u = self._dev(replay[1], (max(nits - 1, 0), W))
+            keep += [dz, u]
+            a.rng_mode = N.OE_RNG_REPLAY
+            a.replay_dz = dz.data_ptr() if nits > 1 else None
+            a.replay_u = u.data_ptr() if nits > 1 else None
+        elif rng == "philox":
+            a.rng_mode = N.OE_RNG_PHILOX
+        else:
+            raise ValueError("rng must be 'replay' or 'philox'")
+        a.theta = theta.data_ptr()
+        a.y0 = y0.data_ptr()
+        a.samples = samples.data_ptr()
+        a.final_stats = final.data_ptr()
+        a.status = status.data_ptr()
+        self._sync_stream()
+        self.ctx.mh_run(a, N.OE_ASYNC)
+        if sync:
+            torch.cuda.synchronize(self.dev)
+        return {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status,
+                "_keep": keep}
+
+    def close(self):
+        self.ctx.close()

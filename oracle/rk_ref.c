@@ -1,0 +1,509 @@
+/*
+ * rk_ref.c — TEST INFRASTRUCTURE ONLY: scalar C restatement of the engine's
+ * integration algorithms, used by tests/ to check the HIP kernels against the
+ * *same* algorithm (the scipy path in cpu_ref.py checks them against the
+ * reference's algorithm).  Never linked into the product.
+ *
+ * What is restated (written independently of odelib_amd/csrc):
+ *   - the demo RHS (Demo_InfectionStates.ipynb:60-128) and the chain model
+ *     (SURVEY App. C), in the notebook's operand order;
+ *   - fixed-step classical RK4 in the operation order of DESIGN.md §3.1
+ *     (compiled with -ffp-contract=off: bitwise equal to the kernel);
+ *   - DOPRI5 with the wavefront rule: walkers 64g..64g+63 share one step size,
+ *     the step error is the max over those lanes of the per-lane max norm
+ *     (DESIGN.md §3.2); equal to the kernel up to libm-vs-ocml pow() ulps;
+ *   - the fused likelihood: chi = Σ finite (O − log C)²/(2S²) (stats.py:41),
+ *     ssres = Σ non-NaN (C − exp O)² (stats.py:52);
+ *   - the batched Metropolis–Hastings step (Samplers.py:104-153) with replay or
+ *     Philox4x32-10 draws.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define LANES 64
+#define MAXS 64
+#define MAXP 80
+
+enum { M_ZERO_I = 0, M_ONE_I = 1, M_TWO_I = 2, M_CHAIN = 3 };
+enum { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4 };
+
+typedef struct {
+  int model, S, P, T;
+  const double* times;
+  int n_obs;
+  const int32_t* obs_tidx; /* sorted ascending */
+  const uint64_t* obs_mask;
+  const double* obs_O;
+  const double* obs_two_s2;
+  const double* obs_lin;
+  int method, substeps, max_steps;
+  double rtol, atol;
+} Prob;
+
+static void rhs(const Prob* pb, const double* y, double t, const double* ps, double* dy) {
+  (void)t;
+  const int N = pb->S;
+  switch (pb->model) {
+    case M_ZERO_I: {
+      double mu = ps[0], phi = ps[1], beta = ps[2];
+      double S = y[0], V = y[1];
+      dy[0] = mu * S - phi * S * V;
+      dy[1] = beta * phi * S * V - phi * S * V;
+      break;
+    }
+    case M_ONE_I: {
+      double mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3];
+      double S = y[0], I1 = y[1], V = y[2];
+      dy[0] = mu * S - phi * S * V;
+      dy[1] = phi * S * V - lam * I1;
+      dy[2] = beta * lam * I1 - phi * S * V;
+      break;
+    }
+    case M_TWO_I: {
+      double mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3], tau = ps[4];
+      double S = y[0], I1 = y[1], I2 = y[2], V = y[3];
+      dy[0] = mu * S - phi * S * V;
+      dy[1] = phi * S * V - tau * I1;
+      dy[2] = tau * I1 - lam * I2;
+      dy[3] = beta * lam * I2 - phi * S * V;
+      break;
+    }
+    default: { /* chain N */
+      double mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3], tau = ps[4];
+      double S = y[0], V = y[N - 1];
+      dy[0] = mu * S - phi * S * V;
+      dy[1] = phi * S * V - tau * y[1];
+      for (int k = 2; k <= N - 3; ++k) dy[k] = tau * y[k - 1] - tau * y[k];
+      dy[N - 2] = tau * y[N - 3] - lam * y[N - 2];
+      dy[N - 1] = beta * lam * y[N - 2] - phi * S * V;
+    }
+  }
+}
+
+typedef struct {
+  double chi, ssres;
+  double ymin; /* min over emitted states (NaN ignored) */
+  int nonfinite;
+  int nvalid, status;
+} Acc;
+
+static void acc_init(Acc* a) {
+  memset(a, 0, sizeof(Acc));
+  a->ymin = INFINITY;
+}
+
+/* status bits: NONFINITE if any emitted state was NaN/inf, NEGATIVE if the minimum
+   emitted state (NaN ignored, -inf counts) was < 0; MAXSTEP from DOPRI5 */
+static int finish(const Acc* a) {
+  int st = a->status;
+  if (a->nonfinite) st |= ST_NONFINITE;
+  if (a->ymin < 0.0) st |= ST_NEGATIVE;
+  return st;
+}
+
+/* output of one walker at grid index i */
+static void emit(const Prob* pb, int i, const double* y, double* traj, int64_t W, int64_t w, int* k, Acc* a) {
+  const int S = pb->S;
+  if (traj)
+    for (int s = 0; s < S; ++s) traj[((int64_t)i * S + s) * W + w] = y[s];
+  for (int s = 0; s < S; ++s) {
+    if (!isfinite(y[s])) a->nonfinite = 1;
+    if (!isnan(y[s]) && y[s] < a->ymin) a->ymin = y[s];
+  }
+  while (*k < pb->n_obs && pb->obs_tidx[*k] == i) {
+    double c = 0.0;
+    for (int s = 0; s < S; ++s)
+      if ((pb->obs_mask[*k] >> s) & 1ull) c = c + y[s];
+    double d = pb->obs_O[*k] - log(c);
+    double term = (d * d) / pb->obs_two_s2[*k];
+    if (isfinite(term)) { a->chi += term; a->nvalid += 1; }
+    double r = c - pb->obs_lin[*k];
+    double r2 = r * r;
+    if (!isnan(r2)) a->ssres += r2;
+    ++*k;
+  }
+}
+
+static int needs_emit(const Prob* pb, int traj, int i, int k) {
+  return traj || (k < pb->n_obs && pb->obs_tidx[k] == i);
+}
+
+/* ---- fixed-step RK4 ---- */
+static void rk4_walker(const Prob* pb, double* y, const double* p, double* traj, int64_t W, int64_t w, Acc* a) {
+  const int S = pb->S;
+  double k[MAXS], acc[MAXS], yt[MAXS];
+  int kk = 0;
+  emit(pb, 0, y, traj, W, w, &kk, a);
+  double t = pb->times[0];
+  const int n = pb->substeps;
+  for (int i = 1; i < pb->T; ++i) {
+    double t1 = pb->times[i];
+    double h = (t1 - t) / (double)n;
+    for (int j = 0; j < n; ++j) {
+      double ts = t + (double)j * h;
+      double hh = 0.5 * h, h6 = h / 6.0;
+      rhs(pb, y, ts, p, k);
+      for (int s = 0; s < S; ++s) { acc[s] = k[s]; yt[s] = fma(hh, k[s], y[s]); }
+      rhs(pb, yt, ts + hh, p, k);
+      for (int s = 0; s < S; ++s) { acc[s] = fma(2.0, k[s], acc[s]); yt[s] = fma(hh, k[s], y[s]); }
+      rhs(pb, yt, ts + hh, p, k);
+      for (int s = 0; s < S; ++s) { acc[s] = fma(2.0, k[s], acc[s]); yt[s] = fma(h, k[s], y[s]); }
+      rhs(pb, yt, ts + h, p, k);
+      for (int s = 0; s < S; ++s) { acc[s] = acc[s] + k[s]; y[s] = fma(h6, acc[s], y[s]); }
+    }
+    t = t1;
+    if (needs_emit(pb, traj != NULL, i, kk)) emit(pb, i, y, traj, W, w, &kk, a);
+  }
+}
+
+/* ---- DOPRI5 over one 64-lane group in lockstep ---- */
+static const double c2 = 1.0 / 5, c3 = 3.0 / 10, c4 = 4.0 / 5, c5 = 8.0 / 9;
+static const double a21 = 1.0 / 5, a31 = 3.0 / 40, a32 = 9.0 / 40, a41 = 44.0 / 45, a42 = -56.0 / 15,
+                    a43 = 32.0 / 9, a51 = 19372.0 / 6561, a52 = -25360.0 / 2187, a53 = 64448.0 / 6561,
+                    a54 = -212.0 / 729, a61 = 9017.0 / 3168, a62 = -355.0 / 33, a63 = 46732.0 / 5247,
+                    a64 = 49.0 / 176, a65 = -5103.0 / 18656, a71 = 35.0 / 384, a73 = 500.0 / 1113,
+                    a74 = 125.0 / 192, a75 = -2187.0 / 6784, a76 = 11.0 / 84;
+static const double e1 = 71.0 / 57600, e3 = -71.0 / 16695, e4 = 71.0 / 1920, e5 = -17253.0 / 339200,
+                    e6 = 22.0 / 525, e7 = -1.0 / 40;
+static const double d1 = -12715105075.0 / 11282082432.0, d3 = 87487479700.0 / 32700410799.0,
+                    d4 = -10690763975.0 / 1880347072.0, d5 = 701980252875.0 / 199316789632.0,
+                    d6 = -1453857185.0 / 822651844.0, d7 = 69997945.0 / 29380423.0;
+
+typedef struct {
+  double y[MAXS], k1[MAXS], k2[MAXS], k3[MAXS], k4[MAXS], k5[MAXS], k6[MAXS], k7[MAXS], yt[MAXS], yn[MAXS];
+  double el;
+  int dead, active;
+  int64_t w;
+  Acc a;
+  int kobs;
+} Lane;
+
+static double grp_max(Lane* L, int n, int use_dead_zero) {
+  double m = 0.0;
+  (void)use_dead_zero;
+  for (int l = 0; l < n; ++l) m = fmax(m, L[l].el);
+  return m;
+}
+
+/* lanes: up to 64; y in L[l].y; p[l*MAXP ...] */
+static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
+  const int S = pb->S;
+  const double t0 = pb->times[0], tend = pb->times[pb->T - 1];
+  const double rtol = pb->rtol, atol = pb->atol;
+  for (int l = 0; l < nl; ++l) {
+    L[l].dead = !L[l].active;
+    L[l].kobs = 0;
+    emit(pb, 0, L[l].y, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
+    rhs(pb, L[l].y, t0, p + l * MAXP, L[l].k1);
+  }
+  double t = t0;
+  /* HINIT per lane, group minimum */
+  double h = INFINITY;
+  for (int l = 0; l < nl; ++l) {
+    Lane* q = &L[l];
+    double d0 = 0.0, d1v = 0.0;
+    for (int s = 0; s < S; ++s) {
+      double sk = atol + rtol * fabs(q->y[s]);
+      d0 = fmax(d0, fabs(q->y[s]) / sk);
+      d1v = fmax(d1v, fabs(q->k1[s]) / sk);
+    }
+    double h0 = (d0 <= 1e-5 || d1v <= 1e-5) ? 1e-6 : 0.01 * (d0 / d1v);
+    h0 = fmin(h0, tend - t0);
+    for (int s = 0; s < S; ++s) q->yt[s] = fma(h0, q->k1[s], q->y[s]);
+    rhs(pb, q->yt, t + h0, p + l * MAXP, q->k2);
+    double d2 = 0.0;
+    for (int s = 0; s < S; ++s) {
+      double sk = atol + rtol * fabs(q->y[s]);
+      d2 = fmax(d2, fabs(q->k2[s] - q->k1[s]) / sk);
+    }
+    d2 = d2 / h0;
+    double dm = fmax(d1v, d2);
+    double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / dm, 0.2);
+    double hl = fmin(100.0 * h0, h1);
+    if (q->dead || !isfinite(hl) || !(hl > 0.0)) hl = tend - t0;
+    h = fmin(h, hl);
+  }
+  h = fmin(h, tend - t0);
+  const double span = tend - t0;
+  const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
+  int i = 1, nst = 0, last_rej = 0;
+  while (i < pb->T) {
+    int last = 0;
+    if (t + h >= tend) { h = tend - t; last = 1; }
+    for (int l = 0; l < nl; ++l) {
+      Lane* q = &L[l];
+      const double* pl = p + l * MAXP;
+      for (int s = 0; s < S; ++s) q->yt[s] = q->y[s] + h * (a21 * q->k1[s]);
+      rhs(pb, q->yt, t + c2 * h, pl, q->k2);
+      for (int s = 0; s < S; ++s) q->yt[s] = q->y[s] + h * (a31 * q->k1[s] + a32 * q->k2[s]);
+      rhs(pb, q->yt, t + c3 * h, pl, q->k3);
+      for (int s = 0; s < S; ++s) q->yt[s] = q->y[s] + h * (a41 * q->k1[s] + a42 * q->k2[s] + a43 * q->k3[s]);
+      rhs(pb, q->yt, t + c4 * h, pl, q->k4);
+      for (int s = 0; s < S; ++s)
+        q->yt[s] = q->y[s] + h * (a51 * q->k1[s] + a52 * q->k2[s] + a53 * q->k3[s] + a54 * q->k4[s]);
+      rhs(pb, q->yt, t + c5 * h, pl, q->k5);
+      for (int s = 0; s < S; ++s)
+        q->yt[s] = q->y[s] + h * (a61 * q->k1[s] + a62 * q->k2[s] + a63 * q->k3[s] + a64 * q->k4[s] + a65 * q->k5[s]);
+      rhs(pb, q->yt, t + h, pl, q->k6);
+      for (int s = 0; s < S; ++s)
+        q->yn[s] = q->y[s] + h * (a71 * q->k1[s] + a73 * q->k3[s] + a74 * q->k4[s] + a75 * q->k5[s] + a76 * q->k6[s]);
+      rhs(pb, q->yn, t + h, pl, q->k7);
+      double el = 0.0;
+      for (int s = 0; s < S; ++s) {
+        double e = h * (e1 * q->k1[s] + e3 * q->k3[s] + e4 * q->k4[s] + e5 * q->k5[s] + e6 * q->k6[s] + e7 * q->k7[s]);
+        double sk = atol + rtol * fmax(fabs(q->y[s]), fabs(q->yn[s]));
+        el = fmax(el, fabs(e) / sk);
+      }
+      if (!isfinite(el)) el = 1e30;
+      if (q->dead) el = 0.0;
+      q->el = el;
+    }
+    double err = grp_max(L, nl, 1);
+    ++nst;
+    if (err <= 1.0) {
+      double tn = last ? tend : t + h;
+      while (i < pb->T && pb->times[i] <= tn) {
+        for (int l = 0; l < nl; ++l) {
+          Lane* q = &L[l];
+          if (!needs_emit(pb, traj != NULL, i, q->kobs)) continue;
+          double yo[MAXS];
+          double ti = pb->times[i];
+          if (ti == tn) {
+            for (int s = 0; s < S; ++s) yo[s] = q->yn[s];
+          } else {
+            double th = (ti - t) / h, th1 = 1.0 - th;
+            for (int s = 0; s < S; ++s) {
+              double ydiff = q->yn[s] - q->y[s];
+              double bspl = h * q->k1[s] - ydiff;
+              double r4 = ydiff - h * q->k7[s] - bspl;
+              double r5 = h * (d1 * q->k1[s] + d3 * q->k3[s] + d4 * q->k4[s] + d5 * q->k5[s] + d6 * q->k6[s] + d7 * q->k7[s]);
+              yo[s] = q->y[s] + th * (ydiff + th1 * (bspl + th * (r4 + th1 * r5)));
+            }
+          }
+          if (q->dead)
+            for (int s = 0; s < S; ++s) yo[s] = NAN;
+          emit(pb, i, yo, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
+        }
+        ++i;
+        nst = 0;
+      }
+      for (int l = 0; l < nl; ++l) {
+        memcpy(L[l].y, L[l].yn, sizeof(double) * S);
+        memcpy(L[l].k1, L[l].k7, sizeof(double) * S);
+      }
+      t = tn;
+      double fac = (err > 0.0) ? 0.9 * pow(err, -0.2) : 10.0;
+      fac = fmin(10.0, fmax(0.2, fac));
+      if (last_rej) fac = fmin(fac, 1.0);
+      h = h * fac;
+      last_rej = 0;
+    } else {
+      h = h * fmax(0.2, 0.9 * pow(err, -0.2));
+      last_rej = 1;
+    }
+    if (nst >= pb->max_steps || h < hmin) {
+      for (int l = 0; l < nl; ++l)
+        if (!L[l].dead && L[l].el >= 0.5 * err) { L[l].dead = 1; L[l].a.status |= ST_MAXSTEP; }
+      nst = pb->max_steps / 2;
+      int alive = 0;
+      for (int l = 0; l < nl; ++l) alive |= !L[l].dead;
+      if (!alive) {
+        double yo[MAXS];
+        for (int s = 0; s < S; ++s) yo[s] = NAN;
+        for (; i < pb->T; ++i)
+          for (int l = 0; l < nl; ++l)
+            if (needs_emit(pb, traj != NULL, i, L[l].kobs))
+              emit(pb, i, yo, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
+        break;
+      }
+      if (h < hmin) h = fmin(1e-3 * span, tend - t);
+    }
+  }
+  for (int l = 0; l < nl; ++l)
+    if (L[l].dead && L[l].active) L[l].a.status |= ST_MAXSTEP;
+}
+
+static Prob make_prob(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
+                      const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
+                      int substeps, double rtol, double atol, int max_steps) {
+  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol};
+  return pb;
+}
+
+/* Integrate walkers [g*64, g*64+64) of a batch; y0/theta/outputs are [..][W]. */
+static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* y0, const double* theta,
+                            double* traj, Acc* out_acc /*[64]*/) {
+  static __thread Lane L[LANES];
+  static __thread double p[LANES * MAXP];
+  const int S = pb->S, P = pb->P;
+  for (int l = 0; l < LANES; ++l) {
+    int64_t gw = g * LANES + l;
+    int active = gw < W;
+    int64_t w = active ? gw : W - 1;
+    L[l].active = active;
+    L[l].w = w;
+    acc_init(&L[l].a);
+    for (int s = 0; s < S; ++s) L[l].y[s] = y0[(int64_t)s * W + w];
+    for (int j = 0; j < MAXP; ++j) p[l * MAXP + j] = (j < P) ? theta[(int64_t)j * W + w] : 0.0;
+  }
+  if (pb->method == 0) {
+    for (int l = 0; l < LANES; ++l)
+      if (L[l].active) rk4_walker(pb, L[l].y, p + l * MAXP, traj, W, L[l].w, &L[l].a);
+  } else {
+    dopri5_group(pb, L, LANES, p, traj, W);
+  }
+  for (int l = 0; l < LANES; ++l) out_acc[l] = L[l].a;
+}
+
+int ref_integrate(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
+                  const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
+                  int substeps, double rtol, double atol, int max_steps, int64_t W, const double* y0,
+                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status) {
+  if (S > MAXS || P > MAXP || W <= 0) return -1;
+  Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
+  Acc acc[LANES];
+  for (int64_t g = 0; g * LANES < W; ++g) {
+    integrate_group(&pb, W, g, y0, theta, traj, acc);
+    for (int l = 0; l < LANES; ++l) {
+      int64_t w = g * LANES + l;
+      if (w >= W) break;
+      if (chi) chi[w] = acc[l].nvalid ? acc[l].chi : NAN;
+      if (ssres) ssres[w] = acc[l].ssres;
+      if (status) status[w] = finish(&acc[l]);
+    }
+  }
+  return 0;
+}
+
+/* ---- Philox4x32-10 (Salmon et al. SC'11; Random123 constants) ---- */
+void ref_philox4x32_10(const uint32_t* ctr_in, const uint32_t* key_in, uint32_t* out) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2v = ctr_in[2], c3v = ctr_in[3];
+  uint32_t k0 = key_in[0], k1 = key_in[1];
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2v;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3v ^ k1;
+    uint32_t n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2v = n2; c3v = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2v; out[3] = c3v;
+}
+
+static double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+/* proposal draws of walker gid at iteration it: z[0..npar) normals, *u uniform */
+void ref_philox_draws(uint64_t seed, uint64_t gid, int it, int npar, double* z, double* u) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t r[4];
+  for (int j = 0; j < npar; j += 2) {
+    uint32_t ctr[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, (uint32_t)(j >> 1)};
+    ref_philox4x32_10(ctr, key, r);
+    double u1 = 1.0 - u53(r[0], r[1]);
+    double u2 = u53(r[2], r[3]);
+    double rad = sqrt(-2.0 * log(u1));
+    double ang = 6.283185307179586 * u2;
+    z[j] = rad * cos(ang);
+    if (j + 1 < npar) z[j + 1] = rad * sin(ang);
+  }
+  uint32_t ctr[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, 0x80000000u};
+  ref_philox4x32_10(ctr, key, r);
+  *u = u53(r[0], r[1]);
+}
+
+/* ---- batched MH (Samplers.py:104-153), groups of 64 walkers in lockstep ---- */
+int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx, const uint64_t* mask,
+           const double* O, const double* two_s2, const double* lin, int method, int substeps, double rtol,
+           double atol, int max_steps, double sstot, int pnum, int64_t W, int64_t walker_offset, int nits, int burnin,
+           int rng_mode, uint64_t seed, double step_sd, const uint8_t* walk, const int32_t* init_param,
+           const double* dz, const double* uu, double* theta /*[P][W] io*/, double* y0 /*[S][W] io*/,
+           double* samples /*[kept][P+5][W]*/, double* final_stats /*[4][W]*/, int32_t* status /*[W]*/) {
+  if (S > MAXS || P > MAXP || W <= 0) return -1;
+  Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
+  int any_walk = 0;
+  for (int j = 0; j < P; ++j) any_walk |= walk[j] != 0;
+  const int PS = P + 5;
+  double* th_new = (double*)malloc(sizeof(double) * P * W);
+  double* y_new = (double*)malloc(sizeof(double) * S * W);
+  double* cur = (double*)malloc(sizeof(double) * 4 * W);
+  double* u_it = (double*)malloc(sizeof(double) * W);
+  Acc acc[LANES];
+  /* a-priori fit */
+  for (int64_t g = 0; g * LANES < W; ++g) {
+    integrate_group(&pb, W, g, y0, theta, NULL, acc);
+    for (int l = 0; l < LANES && g * LANES + l < W; ++l) {
+      int64_t w = g * LANES + l;
+      double c = acc[l].nvalid ? acc[l].chi : NAN;
+      cur[w] = c;
+      cur[W + w] = 1.0 - acc[l].ssres / sstot;
+      cur[2 * W + w] = -2.0 * (-c) + 2.0 * (double)pnum;
+      cur[3 * W + w] = 0.0;
+      status[w] = finish(&acc[l]);
+    }
+  }
+  for (int it = 1; it < nits; ++it) {
+    /* proposals */
+    for (int64_t w = 0; w < W; ++w) {
+      double z[MAXP + 1];
+      double u;
+      if (rng_mode == 0) {
+        for (int j = 0; j < P; ++j) z[j] = dz[((int64_t)(it - 1) * P + j) * W + w];
+        u = uu[(int64_t)(it - 1) * W + w];
+      } else {
+        ref_philox_draws(seed, (uint64_t)(walker_offset + w), it, P + S, z, &u);
+        for (int j = 0; j < P; ++j) z[j] = step_sd * z[j];
+      }
+      u_it[w] = u;
+      for (int j = 0; j < P; ++j) {
+        double v = theta[(int64_t)j * W + w];
+        th_new[(int64_t)j * W + w] = walk[j] ? exp(log(v) + z[j]) : v;
+      }
+      for (int s = 0; s < S; ++s) {
+        int pi = init_param[s];
+        y_new[(int64_t)s * W + w] = (any_walk && pi >= 0) ? th_new[(int64_t)pi * W + w] : y0[(int64_t)s * W + w];
+      }
+    }
+    for (int64_t g = 0; g * LANES < W; ++g) {
+      integrate_group(&pb, W, g, y_new, th_new, NULL, acc);
+      for (int l = 0; l < LANES && g * LANES + l < W; ++l) {
+        int64_t w = g * LANES + l;
+        double chin = acc[l].nvalid ? acc[l].chi : NAN;
+        double lr = exp(cur[w] - chin);
+        double accp = exp(log(lr));
+        if (accp > u_it[w]) {
+          cur[w] = chin;
+          cur[W + w] = 1.0 - acc[l].ssres / sstot;
+          cur[2 * W + w] = -2.0 * (-chin) + 2.0 * (double)pnum;
+          cur[3 * W + w] += 1.0;
+          for (int j = 0; j < P; ++j) theta[(int64_t)j * W + w] = th_new[(int64_t)j * W + w];
+          for (int s = 0; s < S; ++s) y0[(int64_t)s * W + w] = y_new[(int64_t)s * W + w];
+          status[w] = finish(&acc[l]);
+        } else {
+          for (int s = 0; s < S; ++s) {
+            int pi = init_param[s];
+            if (any_walk && pi >= 0) y0[(int64_t)s * W + w] = theta[(int64_t)pi * W + w];
+          }
+        }
+        if (it > burnin) {
+          double* row = samples + (int64_t)(it - burnin - 1) * PS * W + w;
+          for (int j = 0; j < P; ++j) row[(int64_t)j * W] = theta[(int64_t)j * W + w];
+          row[(int64_t)P * W] = cur[w];
+          row[(int64_t)(P + 1) * W] = cur[W + w];
+          row[(int64_t)(P + 2) * W] = cur[2 * W + w];
+          row[(int64_t)(P + 3) * W] = (double)it;
+          row[(int64_t)(P + 4) * W] = cur[3 * W + w] / (double)it;
+        }
+      }
+    }
+  }
+  if (final_stats) memcpy(final_stats, cur, sizeof(double) * 4 * W);
+  free(th_new); free(y_new); free(cur); free(u_it);
+  return 0;
+}

@@ -1,0 +1,120 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes wrapper of oracle/rk_ref.c (see its header).
+
+Batched layouts as in include/odelib_amd.h: y0 [S][W], theta [P][W], traj [T][S][W].
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "build", "librkref.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        vp, i32, i64, d, u64 = C.c_void_p, C.c_int, C.c_int64, C.c_double, C.c_uint64
+        L.ref_integrate.restype = C.c_int
+        L.ref_integrate.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, d, d, i32,
+                                    i64, vp, vp, vp, vp, vp, vp]
+        L.ref_mh.restype = C.c_int
+        L.ref_mh.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, d, d, i32, d, i32,
+                             i64, i64, i32, i32, i32, u64, d, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ref_philox4x32_10.restype = None
+        L.ref_philox4x32_10.argtypes = [vp, vp, vp]
+        L.ref_philox_draws.restype = None
+        L.ref_philox_draws.argtypes = [u64, u64, i32, i32, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+METHODS = {"rk4": 0, "dopri5": 1}
+
+
+class Problem:
+    """Host copy of a FitProblem-like object, observations sorted by grid index
+    (stable), exactly as oe_problem_set orders them."""
+
+    def __init__(self, fp):
+        order = np.argsort(np.asarray(fp.obs_tidx), kind="stable")
+        self.model = int(fp.model_id)
+        self.S, self.P, self.T = int(fp.n_states), int(fp.n_params), len(fp.times)
+        self.times = np.ascontiguousarray(fp.times, dtype=np.float64)
+        self.tidx = np.ascontiguousarray(np.asarray(fp.obs_tidx, np.int32)[order])
+        self.mask = np.ascontiguousarray(np.asarray(fp.obs_mask, np.uint64)[order])
+        self.O = np.ascontiguousarray(np.asarray(fp.obs_log, np.float64)[order])
+        s = np.asarray(fp.obs_logsigma, np.float64)[order]
+        self.two_s2 = np.ascontiguousarray(2.0 * (s * s))
+        self.lin = np.ascontiguousarray(np.asarray(fp.obs_lin, np.float64)[order])
+        self.method = METHODS[fp.method]
+        self.substeps = int(fp.rk4_substeps)
+        self.rtol, self.atol, self.max_steps = float(fp.rtol), float(fp.atol), int(fp.max_steps)
+        self.sstot, self.pnum = float(fp.sstot), int(fp.pnum)
+
+    def args(self):
+        return (self.model, self.S, self.P, self.T, _p(self.times), len(self.tidx), _p(self.tidx),
+                _p(self.mask), _p(self.O), _p(self.two_s2), _p(self.lin), self.method, self.substeps,
+                self.rtol, self.atol, self.max_steps)
+
+
+def integrate(fp, y0, theta, trajectory=True):
+    pr = Problem(fp)
+    y0 = np.ascontiguousarray(y0, dtype=np.float64)
+    theta = np.ascontiguousarray(theta, dtype=np.float64)
+    W = theta.shape[1]
+    traj = np.empty((pr.T, pr.S, W)) if trajectory else None
+    chi = np.empty(W)
+    ssres = np.empty(W)
+    status = np.empty(W, np.int32)
+    rc = lib().ref_integrate(*pr.args(), W, _p(y0), _p(theta), _p(traj), _p(chi), _p(ssres), _p(status))
+    if rc:
+        raise RuntimeError("ref_integrate failed")
+    return {"traj": traj, "chi": chi, "ssres": ssres, "status": status}
+
+
+def mh_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, rng="philox", seed=0, replay=None,
+           step_sd=0.05, walker_offset=0):
+    pr = Problem(fp)
+    theta = np.array(theta, dtype=np.float64, order="C", copy=True)
+    y0 = np.array(y0, dtype=np.float64, order="C", copy=True)
+    W = theta.shape[1]
+    kept = max(0, nits - 1 - burnin)
+    samples = np.empty((max(kept, 1), pr.P + 5, W))
+    final = np.empty((4, W))
+    status = np.zeros(W, np.int32)
+    walk = np.ascontiguousarray(np.asarray(walk_mask, np.uint8))
+    ip = np.full(pr.S, -1, np.int32) if init_param is None else np.ascontiguousarray(np.asarray(init_param, np.int32))
+    dz = u = None
+    if rng == "replay":
+        dz = np.ascontiguousarray(replay[0], dtype=np.float64)
+        u = np.ascontiguousarray(replay[1], dtype=np.float64)
+    rc = lib().ref_mh(*pr.args(), pr.sstot, pr.pnum, W, int(walker_offset), int(nits), int(burnin),
+                      0 if rng == "replay" else 1, int(seed), float(step_sd), _p(walk), _p(ip), _p(dz), _p(u),
+                      _p(theta), _p(y0), _p(samples), _p(final), _p(status))
+    if rc:
+        raise RuntimeError("ref_mh failed")
+    return {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status}
+
+
+def philox4x32_10(ctr, key):
+    c = np.ascontiguousarray(ctr, np.uint32)
+    k = np.ascontiguousarray(key, np.uint32)
+    out = np.empty(4, np.uint32)
+    lib().ref_philox4x32_10(_p(c), _p(k), _p(out))
+    return out
