@@ -1,0 +1,66 @@
+"""Walker sharding across GPUs (one process per GPU) and the posterior all-gather.
+
+The reference's only parallelism is independent chains on a process pool
+(ODElib/Framework.py:755-785, 1025-1030) followed by ``pd.concat`` of the per-chain
+posteriors (Framework.py:1035-1038).  Here chains are walkers: rank r owns the
+contiguous global walker ids ``[offset_r, offset_r + count_r)``, runs them with no
+communication (Philox draws keyed by the GLOBAL id, so the result does not depend on
+the number of GPUs), and the per-rank posterior blocks ``[kept][P+5][count_r]`` are
+pooled by ONE all-gather (RCCL over xGMI with the ``nccl`` backend; gloo on CPU).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard(n_total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous balanced split: (global offset, count) of ``rank``."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    base, extra = divmod(int(n_total), int(world))
+    count = base + (1 if rank < extra else 0)
+    offset = rank * base + min(rank, extra)
+    return offset, count
+
+
+def allgather_walkers(block, n_total: int, group=None):
+    """Gather per-rank blocks [..., count_r] (walker axis last) into [..., n_total] on
+    every rank, in global walker order.  Uneven shards are padded to the largest count
+    for the collective and trimmed afterwards."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    counts = [shard(n_total, r, world)[1] for r in range(world)]
+    cmax = max(counts)
+    lead = tuple(block.shape[:-1])
+    if block.shape[-1] != counts[dist.get_rank(group)]:
+        raise ValueError("block walker count does not match this rank's shard")
+    padded = block
+    if block.shape[-1] < cmax:
+        padded = torch.zeros(lead + (cmax,), dtype=block.dtype, device=block.device)
+        padded[..., :block.shape[-1]] = block
+    padded = padded.contiguous()
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world,) + lead + (cmax,), dtype=block.dtype, device=block.device)
+        dist.all_gather_into_tensor(out, padded, group=group)
+        parts = [out[r, ..., :counts[r]] for r in range(world)]
+    else:
+        bufs = [torch.empty_like(padded) for _ in range(world)]
+        dist.all_gather(bufs, padded, group=group)
+        parts = [bufs[r][..., :counts[r]] for r in range(world)]
+    return torch.cat(parts, dim=-1)
+
+
+def sharded_mh(engine, theta_all, y0_all, nits: int, burnin: int, walk_mask, init_param=None, seed: int = 0,
+               step_sd: float = 0.05, group=None):
+    """Run the global ensemble ``theta_all [P][W_total]`` sharded over the ranks of
+    ``group`` (each rank: its shard on its own device via ``engine``), Philox draws, and
+    return the pooled posterior samples [kept][P+5][W_total] (identical on all ranks)."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    W = int(np.asarray(theta_all).shape[1]) if not hasattr(theta_all, "shape") else int(theta_all.shape[1])
+    off, cnt = shard(W, rank, world)
+    r = engine.mh_run(theta_all[:, off:off + cnt], y0_all[:, off:off + cnt], nits=nits, burnin=burnin,
+                      walk_mask=walk_mask, init_param=init_param, rng="philox", seed=seed, step_sd=step_sd,
+                      walker_offset=off)
+    return allgather_walkers(r["samples"], W, group=group), r

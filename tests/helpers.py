@@ -1,0 +1,107 @@
+"""Shared test helpers: the demo models/priors exactly as the notebook declares them."""
+import os
+
+import numpy as np
+import pandas as pd
+import scipy.stats
+
+from odelib_amd.models import BUILTIN, chain_rhs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+zero_i = BUILTIN["zero_i"][3]
+one_i = BUILTIN["one_i"][3]
+two_i = BUILTIN["two_i"][3]
+
+PRIORS = {
+    "mu": (scipy.stats.lognorm, {"s": 3, "scale": 1e-8}),
+    "phi": (scipy.stats.lognorm, {"s": 3, "scale": 1e-8}),
+    "beta": (scipy.stats.lognorm, {"s": 1, "scale": 20}),
+    "lam": (scipy.stats.lognorm, {"s": 2, "scale": .1}),
+    "tau": (scipy.stats.lognorm, {"s": 2, "scale": 1}),
+}
+THETA = {
+    "zero_i": {"mu": 7.475e-9, "phi": 1.069e-7, "beta": 19.73},
+    "one_i": {"mu": 1.2e-8, "phi": 3.5e-8, "beta": 19.4, "lam": 1.8},
+    "two_i": {"mu": 7.475e-9, "phi": 1.069e-7, "beta": 19.73, "lam": 1.934, "tau": 2.799},
+}
+CONFIGS = {
+    "zero_i": dict(ode=zero_i, pnames=["mu", "phi", "beta"], snames=["S", "V"], rename={"virus": "V", "host": "S"},
+                   sums=None, t_steps=288, extra={}),
+    "one_i": dict(ode=one_i, pnames=["mu", "phi", "beta", "lam"], snames=["S", "I1", "V"],
+                  rename={"virus": "V", "host": "H"}, sums={"H": ["S", "I1"]}, t_steps=1000, extra={"S": 5236900}),
+    "two_i": dict(ode=two_i, pnames=["mu", "phi", "beta", "lam", "tau"], snames=["S", "I1", "I2", "V"],
+                  rename={"virus": "V", "host": "H"}, sums={"H": ["S", "I1", "I2"]}, t_steps=1000,
+                  extra={"S": 5236900}),
+}
+
+
+def demo_df(rename):
+    return pd.read_csv(os.path.join(GOLDEN, "demodata.csv")).replace(rename)
+
+
+def product_model(name, theta=None, seed=0, priors=True, extra_params=None, **engine_kw):
+    """The product's ModelFramework built exactly like make_golden.build_model."""
+    from odelib_amd import ModelFramework, parameter
+    cfg = CONFIGS[name]
+    th = dict(THETA[name] if theta is None else theta)
+    pn = list(cfg["pnames"]) + list((extra_params or {}).keys())
+    kw = {}
+    for p in pn:
+        v = th[p] if p in th else extra_params[p]
+        if priors and p in PRIORS:
+            d, hp = PRIORS[p]
+            kw[p] = parameter(stats_gen=d, hyperparameters=dict(hp), init_value=v)
+        else:
+            kw[p] = parameter(init_value=v)
+    kw.update(cfg["extra"])
+    kw.update(engine_kw)
+    return ModelFramework(ODE=cfg["ode"], parameter_names=pn, state_names=cfg["snames"], dataframe=demo_df(cfg["rename"]),
+                          state_summations=cfg["sums"], t_steps=cfg["t_steps"], random_seed=seed, **kw)
+
+
+def oracle_model(name, theta=None, seed=0, extra_params=None, integrator=None):
+    """oracle.cpu_ref.Model for the same configuration (set-up by the oracle itself)."""
+    from oracle import cpu_ref
+    cfg = CONFIGS[name]
+    df = cpu_ref.format_df(demo_df(cfg["rename"]), cfg["snames"])
+    times = cpu_ref.times_grid(max(df["time"]), cfg["t_steps"])
+    ptidx, olog, osig = cpu_ref.fit_setup(df, times)
+    sidx, out_names, keep, _ = cpu_ref.summation_index(cfg["snames"], cfg["sums"])
+    th = dict(THETA[name] if theta is None else theta)
+    pn = list(cfg["pnames"]) + list((extra_params or {}).keys())
+    params = {}
+    for p in pn:
+        v = th[p] if p in th else extra_params[p]
+        d, hp = PRIORS.get(p, (None, None))
+        params[p] = cpu_ref.Param(v, d, dict(hp) if hp else None)
+    istates = {s: 0 for s in cfg["snames"]}
+    for org, ab in df[df["time"] == 0]["abundance"].items():
+        if org in istates:
+            istates[org] = ab
+    istates.update(cfg["extra"])
+    return cpu_ref.Model(cfg["ode"], pn, cfg["snames"], params, istates, times, ptidx, olog, osig,
+                         sum_index=sidx, sumkeep=keep, out_names=out_names if sidx else cfg["snames"],
+                         random_seed=seed, integrator=integrator)
+
+
+def walker_thetas(name, W=8, seed=0):
+    rs = np.random.RandomState(seed)
+    base = THETA[name]
+    pn = CONFIGS[name]["pnames"]
+    z = rs.standard_normal((W, len(pn)))
+    return np.array([[base[p] * np.exp(0.05 * z[w, j]) for j, p in enumerate(pn)] for w in range(W)])
+
+
+def chain_problem(n, method="rk4", substeps=1, T=1000, **kw):
+    """FitProblem of the synthetic N-state chain with the demo observations (H, V)."""
+    from odelib_amd import ModelFramework, parameter
+    df = demo_df({"virus": "V", "host": "H"})
+    snames = ["S"] + [f"I{k}" for k in range(1, n - 1)] + ["V"]
+    th = THETA["two_i"]
+    m = ModelFramework(ODE=chain_rhs(n), parameter_names=list(th), state_names=snames, dataframe=df,
+                       state_summations={"H": snames[:-1]}, t_steps=T, S=5236900, method=method,
+                       rk4_substeps=substeps, device_model="chain",
+                       **{p: parameter(init_value=v) for p, v in th.items()}, **kw)
+    return m

@@ -1,0 +1,182 @@
+"""CPU tests of the product's host-side logic (no GPU): data set-up parity with the
+reference, the kernel's constant inputs, device-model binding, the replay RNG streams
+and the posterior DataFrame assembly."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from helpers import CONFIGS, THETA, oracle_model, product_model
+from odelib_amd import models
+from odelib_amd import _native as N
+from odelib_amd.rng import legacy_replay_streams
+from odelib_amd.Statistics import Samplers, stats
+from oracle import cpu_ref
+
+MODELS = ["zero_i", "one_i", "two_i"]
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_modelframework_setup_matches_reference(golden, name):
+    m = product_model(name)
+    assert np.array_equal(m.times, golden.setup[f"{name}/times"])
+    assert np.array_equal(np.asarray(m.get_inits(), float), golden.setup[f"{name}/y0"])
+    assert m._pnum == int(golden.setup[f"{name}/pnum"])
+    for s in golden.meta[f"{name}/obs_names"]:
+        assert np.array_equal(m._pred_tindex[s], golden.setup[f"{name}/tidx/{s}"])
+        assert np.array_equal(m._obs_logabundance[s], golden.setup[f"{name}/obs_log/{s}"])
+        assert np.array_equal(m._obs_logsigma[s], golden.setup[f"{name}/obs_logsigma/{s}"])
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_fit_problem_layout(golden, name):
+    """Observation records in get_chi's concatenation order with the summation masks;
+    sstot as stats.Rsqrd computes it."""
+    m = product_model(name)
+    fp = m.fit_problem()
+    names = golden.meta[f"{name}/obs_names"]
+    assert np.array_equal(fp.obs_tidx, np.concatenate([golden.setup[f"{name}/tidx/{s}"] for s in names]))
+    assert np.array_equal(fp.obs_log, np.concatenate([golden.setup[f"{name}/obs_log/{s}"] for s in names]))
+    assert np.array_equal(fp.obs_logsigma, np.concatenate([golden.setup[f"{name}/obs_logsigma/{s}"] for s in names]))
+    # masks: H = S+I1(+I2) for summed models, else the state itself
+    snames = CONFIGS[name]["snames"]
+    sums = CONFIGS[name]["sums"] or {}
+    for k, s in enumerate(np.repeat(names, [len(golden.setup[f"{name}/tidx/{s}"]) for s in names])):
+        group = sums.get(s, [s])
+        assert int(fp.obs_mask[k]) == sum(1 << snames.index(g) for g in group)
+    sstot = 0
+    for s in names:
+        o = np.exp(golden.setup[f"{name}/obs_log/{s}"])
+        sstot += len(o) * np.var(o)
+    assert fp.sstot == sstot
+    assert fp.n_states == len(snames) and fp.n_params == len(CONFIGS[name]["pnames"])
+    # R² from the kernel's ssres form reproduces stats.Rsqrd on the reference predictions
+    for w in range(3):
+        pred = golden.integrate[f"{name}/pred"][w]
+        ssres = np.nansum((pred - fp.obs_lin) ** 2)
+        assert np.isclose(1 - ssres / fp.sstot, golden.integrate[f"{name}/rsq"][w], rtol=1e-12)
+
+
+def test_model_resolution():
+    assert models.resolve(CONFIGS["two_i"]["ode"], 4, 5) == (N.OE_MODEL_TWO_I, 4)
+    assert models.resolve(CONFIGS["one_i"]["ode"], 3, 4) == (N.OE_MODEL_ONE_I, 3)
+    assert models.resolve(CONFIGS["zero_i"]["ode"], 2, 3) == (N.OE_MODEL_ZERO_I, 2)
+    # extra '<state>0' parameters are allowed (P = model P + k)
+    assert models.resolve(CONFIGS["one_i"]["ode"], 3, 5) == (N.OE_MODEL_ONE_I, 3)
+    # two_i IS chain<4>; explicit selection validates the callable
+    assert models.resolve(CONFIGS["two_i"]["ode"], 4, 5, device_model="chain") == (N.OE_MODEL_CHAIN, 4)
+    assert models.resolve(models.chain_rhs(20), 20, 5) == (N.OE_MODEL_CHAIN, 20)
+
+    def zero_i_bad_etiquette(y, t, ps):  # notebook's alternative spelling of zero_i
+        return np.array([ps[0] * y[0] - ps[1] * y[0] * y[1], ps[2] * ps[1] * y[0] * y[1] - ps[1] * y[0] * y[1]])
+    assert models.resolve(zero_i_bad_etiquette, 2, 3) == (N.OE_MODEL_ZERO_I, 2)
+
+    def other(y, t, ps):
+        return np.array([-ps[0] * y[0], ps[1] * y[1]])
+    with pytest.raises(NotImplementedError):
+        models.resolve(other, 2, 3)
+    with pytest.raises(ValueError):
+        models.resolve(other, 2, 3, device_model="zero_i")
+
+
+@pytest.mark.parametrize("key", ["one_i_s7", "two_i_s3", "zero_i_s0_static", "one_i_V0_s5"])
+def test_replay_streams_reproduce_reference_chain(golden, key):
+    """The product's replay stream (rng.py) drives the oracle chain to the reference's
+    posterior bit-exactly: same increments, same uniforms, same consumption."""
+    meta = golden.meta[f"mh/{key}"]
+    m = oracle_model(meta["model"], seed=meta["seed"], extra_params=meta["extra"] or None)
+    pn = m.get_pnames()
+    walking = {p for p in pn if p not in meta["static"]}
+    dists = {p: (m.parameters[p].dist, m.parameters[p].hp) for p in pn}
+    oldvals = [[float(m.parameters[p].val) for p in pn]]
+    dz, u = legacy_replay_streams([meta["seed"]], meta["nits"], pn, walking, dists, oldvals=oldvals)
+    out = cpu_ref.metropolis_hastings(m, nits=meta["nits"], static_parameters=meta["static"],
+                                      replay=(dz[:, :, 0], u[:, 0]))
+    for c in meta["columns"]:
+        assert np.array_equal(out[c], golden.mh[f"{key}/{c}"]), c
+
+
+def test_posterior_frame_layout(golden):
+    """[kept][P+5][W] device block → the reference's MCMC DataFrame layout."""
+    meta = golden.meta["mcmc"]
+    W, kept, P = 3, 19, 4
+    cols = meta["columns"]
+    block = np.zeros((kept, P + 5, W))
+    for w in range(W):
+        rows = golden.mcmc["post/chain#"] == w
+        for j, c in enumerate(cols[:-1]):
+            block[:, j, w] = golden.mcmc[f"post/{c}"][rows]
+    chains = [product_model("one_i") for _ in range(W)]
+    df = Samplers._posterior_frame(block, chains[0].get_pnames(), [], chains, kept)
+    assert list(df.columns) == cols
+    for c in cols:
+        assert np.array_equal(df[c].to_numpy(dtype=float), golden.mcmc[f"post/{c}"]), c
+    assert df["iteration"].dtype == np.int64
+    empty = Samplers._posterior_frame(None, chains[0].get_pnames(), [], chains, 0)
+    assert len(empty) == W and empty.drop(columns=["chain#"]).isna().all().all()
+
+
+def test_lhs_classic_is_stratified():
+    np.random.seed(3)
+    H = Samplers.lhs_classic(4, 50)
+    assert H.shape == (50, 4)
+    for j in range(4):
+        assert np.array_equal(np.sort(np.floor(H[:, j] * 50)), np.arange(50))
+
+
+def test_stats_formulas_match_oracle(golden):
+    rs = np.random.RandomState(1)
+    O, C, S = rs.rand(37) + 1, rs.rand(37) + 1, rs.rand(37) + 0.1
+    C[3] = np.nan
+    assert stats.chi(O, C, S) == cpu_ref.chi(O, C, S)
+    assert stats.AIC(3.5, 5) == cpu_ref.aic(3.5, 5)
+    d = {"H": rs.rand(18), "V": rs.rand(19)}
+    o = {"H": rs.rand(18), "V": rs.rand(19)}
+    assert stats.Rsqrd(d, o) == cpu_ref.rsqrd(d, o)
+    assert np.isclose(stats.get_adjusted_rsquared(0.9, 37, 5), 1 - 0.1 * 36 / 31)
+
+
+def test_parameter_api():
+    import scipy.stats
+    from odelib_amd import parameter
+    p = parameter(stats_gen=scipy.stats.lognorm, hyperparameters={"s": 1, "scale": 2.0}, init_value=3.0)
+    assert p.has_distribution() and float(p.val) == 3.0
+    q = p.copy()
+    assert q.dist is p.dist and float(q.val) == 3.0
+    np.random.seed(0)
+    p.rwalk()
+    np.random.seed(0)
+    assert float(p.val) == float(np.exp(np.log(3.0) + np.random.normal(0, 0.05)))
+    with pytest.raises(ValueError):
+        parameter()
+    r = parameter(init_value=2.0)
+    assert not r.has_distribution() and r.pdf() == 1.0
+    f = parameter(stats_gen=scipy.stats.norm, hyperparameters={}, init_value=1.0)
+    f.fit(np.random.RandomState(0).normal(5.0, 2.0, 2000))
+    assert abs(f.hp["loc"] - 5.0) < 0.2 and abs(f.hp["scale"] - 2.0) < 0.2
+
+
+def test_engine_options_do_not_shadow_names():
+    m = product_model("two_i", method="rk4", rk4_substeps=2)
+    assert m.method == "rk4" and m.rk4_substeps == 2
+    fp = m.fit_problem()
+    assert fp.method == "rk4" and fp.rk4_substeps == 2
+    m2 = m.copy(overwrite={"mu": 1e-8, "S": 5.0})
+    assert float(m2.parameters["mu"].val) == 1e-8 and m2.istates["S"] == 5.0
+    assert float(m.parameters["mu"].val) == THETA["two_i"]["mu"]
+    with pytest.raises(Exception):
+        m.set_parameters(nope=1.0)
+    with pytest.raises(Exception):
+        m.set_inits(nope=1.0)
+    assert "Current State Summations" in repr(m)
+
+
+def test_compute_without_gpu_fails_loudly():
+    """No CPU fallback: on a machine without a HIP device every compute call raises."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is present")
+    m = product_model("two_i")
+    with pytest.raises(N.NativeUnavailable):
+        m.integrate()
+    with pytest.raises(N.NativeUnavailable):
+        m.MCMC(chain_inits=[THETA["two_i"]], iterations_per_chain=4, print_report=False)

@@ -1,0 +1,103 @@
+"""Pin the oracle (oracle/cpu_ref.py) against golden vectors produced by the reference
+itself (tests/golden/make_golden.py).  Everything here is bit-exact: the oracle issues
+the same scipy/numpy calls in the same order as ODElib."""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+
+from helpers import CONFIGS, THETA, demo_df, oracle_model
+from oracle import cpu_ref
+
+MODELS = ["zero_i", "one_i", "two_i"]
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_setup_matches_reference(golden, name):
+    cfg = CONFIGS[name]
+    df = cpu_ref.format_df(demo_df(cfg["rename"]), cfg["snames"])
+    times = cpu_ref.times_grid(max(df["time"]), cfg["t_steps"])
+    assert np.array_equal(times, golden.setup[f"{name}/times"])
+    ptidx, olog, osig = cpu_ref.fit_setup(df, times)
+    for s in golden.meta[f"{name}/obs_names"]:
+        assert np.array_equal(ptidx[s], golden.setup[f"{name}/tidx/{s}"])
+        assert np.array_equal(olog[s], golden.setup[f"{name}/obs_log/{s}"])
+        assert np.array_equal(osig[s], golden.setup[f"{name}/obs_logsigma/{s}"])
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_integrate_and_fit_stats_bit_exact(golden, name):
+    m = oracle_model(name)
+    TH = golden.integrate[f"{name}/theta"]
+    y0 = [m.istates[s] for s in CONFIGS[name]["snames"]]
+    assert np.array_equal(np.asarray(y0, float), golden.setup[f"{name}/y0"])
+    for w in range(TH.shape[0]):
+        traj = cpu_ref.odeint_traj(CONFIGS[name]["ode"], y0, m.times, TH[w])
+        assert np.array_equal(traj, golden.integrate[f"{name}/traj"][w])
+        for p, v in zip(m._pnames, TH[w]):
+            m.parameters[p].val = np.array(v)
+        d = m.integrate_obs()
+        assert np.array_equal(np.concatenate([d[s] for s in d]), golden.integrate[f"{name}/pred"][w])
+        c = m.get_chi(d)
+        assert float(c) == golden.integrate[f"{name}/chi"][w]
+        assert float(m.get_Rsqrd(d)) == golden.integrate[f"{name}/rsq"][w]
+        assert float(m.get_AIC(c)) == golden.integrate[f"{name}/aic"][w]
+
+
+def _chain_cfg(golden, key):
+    meta = golden.meta[f"mh/{key}"]
+    return meta, {c: golden.mh[f"{key}/{c}"] for c in meta["columns"]}
+
+
+@pytest.mark.parametrize("key", ["one_i_s7", "two_i_s3", "zero_i_s0_static", "one_i_V0_s5"])
+def test_metropolis_hastings_bit_exact(golden, key):
+    meta, ref = _chain_cfg(golden, key)
+    m = oracle_model(meta["model"], seed=meta["seed"], extra_params=meta["extra"] or None)
+    out = cpu_ref.metropolis_hastings(m, nits=meta["nits"], static_parameters=meta["static"])
+    for c in meta["columns"]:
+        assert np.array_equal(out[c], ref[c]), c
+
+
+def test_mcmc_pooling_and_rawstats(golden):
+    meta = golden.meta["mcmc"]
+    cols = [c for c in meta["columns"] if c != "chain#"]
+    outs = []
+    for i, init in enumerate(meta["inits"]):
+        m = oracle_model("one_i", theta=init, seed=i)
+        o = cpu_ref.metropolis_hastings(m, nits=meta["iterations"], burnin=int(meta["iterations"] / 2))
+        o["chain#"] = np.full(len(o["chi"]), i, float)
+        outs.append(o)
+    for c in cols + ["chain#"]:
+        assert np.array_equal(np.concatenate([o[c] for o in outs]), golden.mcmc[f"post/{c}"]), c
+    import pandas as pd
+    for p in ["mu", "phi", "beta", "lam"]:
+        med, std = cpu_ref.rawstats(pd.Series(golden.mcmc[f"post/{p}"]))
+        assert np.array_equal([med, std], golden.mcmc[f"rawstats/{p}"])
+
+
+def test_replicate_dataframe_setup(golden):
+    import os
+
+    import pandas as pd
+    from helpers import GOLDEN
+    rdf = pd.read_csv(os.path.join(GOLDEN, "replicate_data.csv"))
+    df = cpu_ref.format_df(rdf, ["S", "I1", "V"])
+    times = cpu_ref.times_grid(max(df["time"]), 100)
+    assert np.array_equal(times, golden.replicate["times"])
+    ptidx, olog, osig = cpu_ref.fit_setup(df, times)
+    for s in ptidx:
+        assert np.array_equal(ptidx[s], golden.replicate[f"tidx/{s}"])
+        assert np.array_equal(olog[s], golden.replicate[f"obs_log/{s}"])
+        assert np.array_equal(osig[s], golden.replicate[f"obs_logsigma/{s}"])
+
+
+def test_masked_chi_semantics():
+    """stats.chi drops non-finite terms (stats.py:41); all-masked is np.ma.masked."""
+    O = np.array([1., 2., 3., 4.])
+    assert float(cpu_ref.chi(O, np.array([1.5, np.nan, np.inf, -np.inf]), np.ones(4))) == 0.125
+    assert cpu_ref.chi(O, np.full(4, np.nan), np.ones(4)) is np.ma.masked
+    assert float(cpu_ref.chi(O, np.array([1., 2, 3, 4.5]), np.array([0., 1, 1, 1]))) == 0.125
+    # an all-masked proposal is never accepted (acc > u is masked -> falsy)
+    acc = np.exp(0.0 - cpu_ref.chi(O, np.full(4, np.nan), np.ones(4)))
+    assert not bool(acc > 0.5)
