@@ -46,7 +46,36 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mcmc-iters", type=int, default=21, help="MCMC leg iterations (0 = skip)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
     return ap.parse_args()
+
+
+def workload_args(args):
+    out = ["--model", args.model, "--method", args.method, "--walkers", str(args.walkers), "--times", str(args.times)]
+    if args.cached_stores:
+        out.append("--cached-stores")
+    return out
+
+
+def pmc_traffic(args):
+    """HBM bytes per dispatch of the integrate kernel from two separate rocprofv3 PMC
+    passes (FETCH_SIZE, WRITE_SIZE) of this same workload, run as child processes
+    before this process touches the GPU.  gfx950 correction: FETCH_SIZE x2
+    (MI355X_MICROARCH.md §HBM).  Returns (bytes or None, note)."""
+    import shutil
+    import tempfile
+    if shutil.which("rocprofv3") is None:
+        return None, "rocprofv3 not found"
+    try:
+        from tools.profile import pmc_pass
+        out = tempfile.mkdtemp(prefix="bench_pmc_", dir=os.path.join(ROOT, "gpurun_out")
+                               if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None)
+        wl = workload_args(args) + ["--no-pmc"]
+        f = pmc_pass(out, "FETCH_SIZE", wl + ["--steps", "3", "--warmup", "1"], "k_integrate", 240)
+        w = pmc_pass(out, "WRITE_SIZE", wl + ["--steps", "3", "--warmup", "1"], "k_integrate", 240)
+        return f["mean"] * 1024 * 2 + w["mean"] * 1024, f"rocprofv3 PMC FETCH_SIZE(x2)+WRITE_SIZE, {f['dispatches']} dispatches"
+    except BaseException as e:  # never let profiling break the bench line
+        return None, f"PMC pass failed: {e!r}"[:200]
 
 
 def build_problem(model: str, method: str, T: int):
@@ -143,6 +172,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.model, fp_host, y0h, args.cpu_seconds, P)
+    traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
+    if world == 1 and not args.no_pmc:
+        traffic, traffic_note = pmc_traffic(args)
 
     import numpy as np
     import torch
@@ -241,7 +273,7 @@ def main():
                        "walkers_per_gpu": Wl, "walkers_total": Wl * n_gpus, "states": S, "times": T,
                        "method": args.method, "stores": "cached" if args.cached_stores else "nontemporal", "parallelism": f"walker-shard x{n_gpus}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_s * 1e3, "bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "mcmc": mcmc,

@@ -1,0 +1,120 @@
+"""Profile the bench workload with rocprofv3 (run on the GPU box).
+
+    python tools/profile.py --tag r01 [bench args...]
+
+1. kernel trace + stats      rocprofv3 --kernel-trace --stats
+2. PMC pass FETCH_SIZE       rocprofv3 --pmc FETCH_SIZE   (own pass: 3 TCC slots)
+3. PMC pass WRITE_SIZE       rocprofv3 --pmc WRITE_SIZE   (own pass: 2 TCC slots)
+
+Each pass runs ``python3 bench.py`` directly after ``--`` (no launcher hops).  Outputs
+go to gpurun_out/prof_<tag>/; the summary (per-kernel mean duration, HBM bytes per
+dispatch with the gfx950 FETCH_SIZE ×2 correction of MI355X_MICROARCH.md §HBM) is
+written to gpurun_out/prof_<tag>/<tag>_summary.json with the stats CSV; copy both into
+profiles/ (tracked) to commit them.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rocprof():
+    """rocprofv3 is a `#!/usr/bin/env python3` script: run it with this interpreter so no
+    env -> python3 exec hop happens in the process tree."""
+    path = shutil.which("rocprofv3")
+    if path is None:
+        raise SystemExit("rocprofv3 not found")
+    return [sys.executable, path]
+
+
+def run(cmd, timeout):
+    print("+", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, cwd=ROOT, timeout=timeout, capture_output=True, text=True)
+    tail = (r.stdout[-2000:] + r.stderr[-2000:])
+    if r.returncode != 0:
+        print(tail)
+        raise SystemExit(f"command failed ({r.returncode})")
+    return r.stdout
+
+
+def find(pattern):
+    hits = sorted(glob.glob(pattern, recursive=True))
+    return hits[0] if hits else None
+
+
+def read_csv(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def pmc_pass(out, counter, bench_args, kernel_regex, timeout):
+    d = os.path.join(out, f"pmc_{counter.lower()}")
+    run(rocprof() + ["--pmc", counter, "--kernel-include-regex", kernel_regex, "--output-format", "csv",
+         "-d", d, "-o", "run", "--", sys.executable, "bench.py", "--no-cpu-baseline", "--mcmc-iters", "0",
+         "--steps", "5", "--warmup", "1", *bench_args], timeout)
+    path = find(os.path.join(d, "**", "*counter_collection.csv"))
+    rows = read_csv(path)
+    vals = {}
+    for r in rows:
+        if r.get("Counter_Name") != counter:
+            continue
+        key = (r.get("Dispatch_Id"), r.get("Kernel_Name"))
+        vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])  # sum over XCD / instances
+    per = list(vals.values())
+    return {"dispatches": len(per), "mean": sum(per) / max(len(per), 1), "csv": os.path.relpath(path, ROOT)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--kernel-regex", default="k_integrate")
+    ap.add_argument("--timeout", type=int, default=300)
+    ap.add_argument("--skip-pmc", action="store_true")
+    args, bench_args = ap.parse_known_args()
+    out = os.path.join(ROOT, "gpurun_out", f"prof_{args.tag}")
+    os.makedirs(out, exist_ok=True)
+
+    # 1. kernel trace + stats (same command line as the bench run, minus the CPU leg)
+    d = os.path.join(out, "trace")
+    stdout = run(rocprof() + ["--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run", "--",
+                  sys.executable, "bench.py", "--no-cpu-baseline", *bench_args], args.timeout)
+    bench_line = [l for l in stdout.splitlines() if l.startswith("{")]
+    stats_csv = find(os.path.join(d, "**", "*kernel_stats.csv"))
+    stats = read_csv(stats_csv)
+    shutil.copyfile(stats_csv, os.path.join(out, f"{args.tag}_kernel_stats.csv"))
+    summary = {"tag": args.tag, "bench_args": bench_args, "kernels": []}
+    for r in stats:
+        summary["kernels"].append({k: r[k] for k in r})
+    summary["bench_line_under_profiler"] = json.loads(bench_line[-1]) if bench_line else None
+
+    # 2./3. HBM traffic per dispatch of the hot kernel, separate PMC passes
+    if not args.skip_pmc:
+        fetch = pmc_pass(out, "FETCH_SIZE", bench_args, args.kernel_regex, args.timeout)
+        write = pmc_pass(out, "WRITE_SIZE", bench_args, args.kernel_regex, args.timeout)
+        # units: kilobytes; gfx950 FETCH_SIZE reads half the bytes of a wide coalesced
+        # stream (MI355X_MICROARCH.md §HBM) -> x2
+        fetch_b = fetch["mean"] * 1024 * 2
+        write_b = write["mean"] * 1024
+        summary["pmc"] = {"kernel_regex": args.kernel_regex, "FETCH_SIZE_kB_raw": fetch["mean"],
+                          "WRITE_SIZE_kB": write["mean"], "fetch_bytes_corrected": fetch_b,
+                          "write_bytes": write_b, "hbm_bytes_per_dispatch": fetch_b + write_b,
+                          "dispatches": [fetch["dispatches"], write["dispatches"]],
+                          "csv": [fetch["csv"], write["csv"]]}
+    # written under gpurun_out/ (merged back by gpurun); copy into profiles/ to commit
+    with open(os.path.join(out, f"{args.tag}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps(summary.get("pmc"), indent=1))
+    for k in summary["kernels"]:
+        print({kk: k[kk] for kk in k if kk in ("Name", "Calls", "AverageNs", "TotalDurationNs", "Percentage")})
+
+
+if __name__ == "__main__":
+    main()
