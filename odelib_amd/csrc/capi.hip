@@ -56,6 +56,8 @@ const Entry* find_entry(int32_t model_id, int32_t S) {
 }
 
 constexpr int kBlock = 256;
+// per-lane store offsets are 32-bit byte offsets (w*8) into a [..][W] row
+constexpr int64_t kMaxWalkers = int64_t(1) << 29;
 
 }  // namespace
 
@@ -278,7 +280,7 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
                  double* chi, double* ssres, int32_t* status, uint32_t flags) {
   if (!c || !c->own_stream) return OE_ERR_STATE;
   if (!c->has_problem) return fail(c, OE_ERR_STATE, "oe_integrate: call oe_problem_set first");
-  if (W <= 0) return fail(c, OE_ERR_ARG, "oe_integrate: n_walkers must be > 0");
+  if (W <= 0 || W > kMaxWalkers) return fail(c, OE_ERR_ARG, "oe_integrate: n_walkers must be in [1, 2^29]");
   if (!y0 || !theta) return fail(c, OE_ERR_ARG, "oe_integrate: y0 and theta are required");
   int rc = set_device(c);
   if (rc) return rc;
@@ -286,6 +288,8 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   const int S = e->S, P = c->dp.P, T = c->dp.T;
   const bool host = flags & OE_HOST_PTRS;
   const bool nt = flags & OE_NT_STORES;
+  if (traj && (int64_t)S * W * 8 >= (int64_t(1) << 32))
+    return fail(c, OE_ERR_ARG, "oe_integrate: one trajectory row (S*W*8 bytes) must be < 4 GiB");
 
   IntegrateArgs ia{};
   ia.W = W;
@@ -343,7 +347,7 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   const Entry* e = c->entry;
   const int S = e->S, P = c->dp.P;
   const int64_t W = a->n_walkers;
-  if (W <= 0) return fail(c, OE_ERR_ARG, "oe_mh_run: n_walkers must be > 0");
+  if (W <= 0 || W > kMaxWalkers) return fail(c, OE_ERR_ARG, "oe_mh_run: n_walkers must be in [1, 2^29]");
   if (a->nits < 1) return fail(c, OE_ERR_ARG, "oe_mh_run: nits must be >= 1");
   if (a->burnin < 0) return fail(c, OE_ERR_ARG, "oe_mh_run: burnin must be >= 0");
   if (!a->theta || !a->y0 || !a->walk_mask || !a->init_param)

@@ -97,32 +97,50 @@ __device__ __forceinline__ double pick(const double (&a)[N], int idx) {
   return v;
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// Store one trajectory row element through a buffer resource: descriptor (row base,
+// row bytes) in SGPRs, lane offset w*8 in one VGPR, state offset s*W*8 in an SGPR —
+// no per-store 64-bit VALU address arithmetic.  aux = 2 sets the non-temporal bit.
 template <bool NT>
-__device__ __forceinline__ void st(double* p, double v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+__device__ __forceinline__ void st_row(__amdgpu_buffer_rsrc_t rsrc, uint32_t lane_off, uint32_t s_off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rsrc, lane_off, s_off, NT ? 2 : 0);
 }
 
-// Emit grid point i: store the trajectory row (TRAJ), flag status, and fold every
-// observation recorded at grid index i into the likelihood.  `k` is the
-// wave-uniform observation cursor.
+// NaN-propagating finiteness accumulator: a.nf becomes NaN iff some y[s] is NaN/inf.
+template <int S>
+__device__ __forceinline__ void check_finite(const double (&y)[S], Acc& a) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) a.nf = fma(y[s], 0.0, a.nf);
+}
+
+// Store grid row i of the trajectory (TRAJ) and track the minimum state.  `off` is
+// the lane's byte offset w*8 (32-bit); rows are stored through a per-row buffer
+// descriptor (S*W*8 < 2^32, checked on the host): no per-store VALU address math.
 template <int S, bool TRAJ, bool NT>
-__device__ __forceinline__ void emit(const DevProblem& pb, int i, const double (&y)[S],
-                                     double* __restrict__ traj, int64_t W, int64_t w,
-                                     bool active, int& k, Acc& a) {
+__device__ __forceinline__ void store_row(int i, const double (&y)[S], double* __restrict__ traj,
+                                          int64_t W, uint32_t off, bool active, Acc& a) {
   if constexpr (TRAJ) {
     if (active) {
-      double* row = traj + (int64_t)i * S * W + w;
+      const uint32_t row_bytes = (uint32_t)(S * W * 8);
+      const __amdgpu_buffer_rsrc_t rsrc =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(traj + (int64_t)i * S * W), 0, row_bytes, 0x00020000);
 #pragma unroll
-      for (int s = 0; s < S; ++s) st<NT>(row + (int64_t)s * W, y[s]);
+      for (int s = 0; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
     }
   }
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    a.nf = fma(y[s], 0.0, a.nf);
-    a.ymin = fmin(a.ymin, y[s]);
-  }
+  for (int s = 0; s < S; ++s) a.ymin = fmin(a.ymin, y[s]);
+}
+
+// Fold every observation recorded at grid index i into the likelihood (caller knows
+// one exists or checks `k`).  Finiteness is checked here and at the final state
+// (NaN/inf propagate through the RHS), not at every step.
+template <int S>
+__device__ __forceinline__ void observe(const DevProblem& pb, int i, const double (&y)[S], int& k, Acc& a) {
   const cptr<Obs> obs = kconst(pb.obs);
+  if (!(k < pb.n_obs && obs[k].tidx == i)) return;
+  check_finite(y, a);
   while (k < pb.n_obs && obs[k].tidx == i) {
     const uint64_t mask = obs[k].mask;
     const double O = obs[k].O, two_s2 = obs[k].two_s2, O_lin = obs[k].O_lin;
@@ -140,6 +158,15 @@ __device__ __forceinline__ void emit(const DevProblem& pb, int i, const double (
     if (!__builtin_isnan(r2)) a.ssres += r2;
     ++k;
   }
+}
+
+// Emit grid point i: row store + minimum + observations.
+template <int S, bool TRAJ, bool NT>
+__device__ __forceinline__ void emit(const DevProblem& pb, int i, const double (&y)[S],
+                                     double* __restrict__ traj, int64_t W, uint32_t off,
+                                     bool active, int& k, Acc& a) {
+  store_row<S, TRAJ, NT>(i, y, traj, W, off, active, a);
+  observe<S>(pb, i, y, k, a);
 }
 
 template <int S, bool TRAJ>
@@ -178,19 +205,34 @@ __device__ __forceinline__ void rk4_step(double (&y)[M::S], double t, double h, 
 template <class M, int PMAX, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[M::S],
                                               const double (&p)[PMAX], double* traj,
-                                              int64_t W, int64_t w, bool active, Acc& a) {
+                                              int64_t W, uint32_t off, bool active, Acc& a) {
   int k = 0;
-  emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, w, active, k, a);
+  emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
   const int n = pb.substeps;
   const cptr<double> tab = kconst(pb.rk4);
-  for (int i = 1; i < pb.T; ++i) {
-    // per-interval constants, computed on the host exactly as written here:
-    // h = (t_i - t_{i-1}) / n, hh = 0.5*h, h6 = h/6
+  const cptr<Obs> obs = kconst(pb.obs);
+  // one output interval: per-interval constants computed on the host exactly as
+  // h = (t_i - t_{i-1}) / n, hh = 0.5*h, h6 = h/6; substep j starts at t_{i-1} + j*h
+  auto interval = [&](int i) {
     const double h = tab[4 * (i - 1)], hh = tab[4 * (i - 1) + 1], h6 = tab[4 * (i - 1) + 2];
     const double t = tab[4 * (i - 1) + 3];
     for (int j = 0; j < n; ++j) rk4_step<M, PMAX>(y, t + (double)j * h, h, hh, h6, p);
-    if (grid_needs_emit<M::S, TRAJ>(pb, i, k)) emit<M::S, TRAJ, NT>(pb, i, y, traj, W, w, active, k, a);
+  };
+  int i = 1;
+  while (i < pb.T) {
+    // observation-free segment [i, next): step + row store only (no per-step obs logic)
+    const int next = (k < pb.n_obs) ? obs[k].tidx : pb.T;
+    for (; i < next; ++i) {
+      interval(i);
+      if constexpr (TRAJ) store_row<M::S, TRAJ, NT>(i, y, traj, W, off, active, a);
+    }
+    if (i < pb.T) {  // i == next: an observed grid point
+      interval(i);
+      emit<M::S, TRAJ, NT>(pb, i, y, traj, W, off, active, k, a);
+      ++i;
+    }
   }
+  check_finite(y, a);
 }
 
 // ---------------------------------------------------------------------------------
@@ -222,11 +264,11 @@ constexpr double safe = 0.9, facmin = 0.2, facmax = 10.0;
 template <class M, int PMAX, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
-                                                 int64_t W, int64_t w, bool active, Acc& a) {
+                                                 int64_t W, uint32_t off, bool active, Acc& a) {
   using namespace dp;
   constexpr int S = M::S;
   int k = 0;
-  emit<S, TRAJ, NT>(pb, 0, y, traj, W, w, active, k, a);
+  emit<S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
   const cptr<double> times = kconst(pb.times);
   const double t0 = times[0];
   const double tend = times[pb.T - 1];
@@ -336,7 +378,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
             for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
           }
-          emit<S, TRAJ, NT>(pb, i, yo, traj, W, w, active, k, a);
+          emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
         }
         ++i;
         nst = 0;
@@ -364,21 +406,23 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
         for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
         for (; i < pb.T; ++i)
-          if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, w, active, k, a);
+          if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
         break;
       }
       if (h < hmin) h = fmin(1e-3 * span, tend - t);
     }
   }
   if (dead && active) a.status |= ST_MAXSTEP;
+  check_finite(y, a);
 }
 
 template <class M, int PMAX, int METHOD, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, int64_t w, bool active, Acc& a) {
-  if constexpr (METHOD == 0) integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, w, active, a);
-  else integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, w, active, a);
+  const uint32_t off = (uint32_t)w * 8u;  // byte offset of walker w in a [..][W] row
+  if constexpr (METHOD == 0) integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  else integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
 }
 
 // ---------------------------------------------------------------------------------

@@ -6,7 +6,7 @@
  *
  * What is restated (written independently of odelib_amd/csrc):
  *   - the demo RHS (Demo_InfectionStates.ipynb:60-128) and the chain model
- *     (SURVEY App. C), in the notebook's operand order;
+ *     (SURVEY App. C), each a*b - c*d evaluated as fma(a, b, -(c*d));
  *   - fixed-step classical RK4 in the operation order of DESIGN.md §3.1
  *     (compiled with -ffp-contract=off: bitwise equal to the kernel);
  *   - DOPRI5 with the wavefront rule: walkers 64g..64g+63 share one step size,
@@ -49,35 +49,39 @@ static void rhs(const Prob* pb, const double* y, double t, const double* ps, dou
     case M_ZERO_I: {
       double mu = ps[0], phi = ps[1], beta = ps[2];
       double S = y[0], V = y[1];
-      dy[0] = mu * S - phi * S * V;
-      dy[1] = beta * phi * S * V - phi * S * V;
+      double inf = phi * S * V;
+      dy[0] = fma(mu, S, -inf);
+      dy[1] = fma(beta, inf, -inf);
       break;
     }
     case M_ONE_I: {
       double mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3];
       double S = y[0], I1 = y[1], V = y[2];
-      dy[0] = mu * S - phi * S * V;
-      dy[1] = phi * S * V - lam * I1;
-      dy[2] = beta * lam * I1 - phi * S * V;
+      double inf = phi * S * V;
+      dy[0] = fma(mu, S, -inf);
+      dy[1] = fma(-lam, I1, inf);
+      dy[2] = fma(beta * lam, I1, -inf);
       break;
     }
     case M_TWO_I: {
       double mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3], tau = ps[4];
       double S = y[0], I1 = y[1], I2 = y[2], V = y[3];
-      dy[0] = mu * S - phi * S * V;
-      dy[1] = phi * S * V - tau * I1;
-      dy[2] = tau * I1 - lam * I2;
-      dy[3] = beta * lam * I2 - phi * S * V;
+      double inf = phi * S * V;
+      dy[0] = fma(mu, S, -inf);
+      dy[1] = fma(-tau, I1, inf);
+      dy[2] = fma(tau, I1, -(lam * I2));
+      dy[3] = fma(beta * lam, I2, -inf);
       break;
     }
     default: { /* chain N */
       double mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3], tau = ps[4];
       double S = y[0], V = y[N - 1];
-      dy[0] = mu * S - phi * S * V;
-      dy[1] = phi * S * V - tau * y[1];
-      for (int k = 2; k <= N - 3; ++k) dy[k] = tau * y[k - 1] - tau * y[k];
-      dy[N - 2] = tau * y[N - 3] - lam * y[N - 2];
-      dy[N - 1] = beta * lam * y[N - 2] - phi * S * V;
+      double inf = phi * S * V;
+      dy[0] = fma(mu, S, -inf);
+      dy[1] = fma(-tau, y[1], inf);
+      for (int k = 2; k <= N - 3; ++k) dy[k] = fma(tau, y[k - 1], -(tau * y[k]));
+      dy[N - 2] = fma(tau, y[N - 3], -(lam * y[N - 2]));
+      dy[N - 1] = fma(beta * lam, y[N - 2], -inf);
     }
   }
 }
@@ -103,15 +107,20 @@ static int finish(const Acc* a) {
   return st;
 }
 
+static void check_finite(int S, const double* y, Acc* a) {
+  for (int s = 0; s < S; ++s)
+    if (!isfinite(y[s])) a->nonfinite = 1;
+}
+
 /* output of one walker at grid index i */
 static void emit(const Prob* pb, int i, const double* y, double* traj, int64_t W, int64_t w, int* k, Acc* a) {
   const int S = pb->S;
   if (traj)
     for (int s = 0; s < S; ++s) traj[((int64_t)i * S + s) * W + w] = y[s];
-  for (int s = 0; s < S; ++s) {
-    if (!isfinite(y[s])) a->nonfinite = 1;
+  for (int s = 0; s < S; ++s)
     if (!isnan(y[s]) && y[s] < a->ymin) a->ymin = y[s];
-  }
+  /* finiteness is checked at observation points and at the final state */
+  if (*k < pb->n_obs && pb->obs_tidx[*k] == i) check_finite(S, y, a);
   while (*k < pb->n_obs && pb->obs_tidx[*k] == i) {
     double c = 0.0;
     for (int s = 0; s < S; ++s)
@@ -156,6 +165,7 @@ static void rk4_walker(const Prob* pb, double* y, const double* p, double* traj,
     t = t1;
     if (needs_emit(pb, traj != NULL, i, kk)) emit(pb, i, y, traj, W, w, &kk, a);
   }
+  check_finite(S, y, a);
 }
 
 /* ---- DOPRI5 over one 64-lane group in lockstep ---- */
@@ -321,8 +331,10 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
       if (h < hmin) h = fmin(1e-3 * span, tend - t);
     }
   }
-  for (int l = 0; l < nl; ++l)
+  for (int l = 0; l < nl; ++l) {
     if (L[l].dead && L[l].active) L[l].a.status |= ST_MAXSTEP;
+    check_finite(S, L[l].y, &L[l].a);
+  }
 }
 
 static Prob make_prob(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
