@@ -233,6 +233,7 @@ def main():
         nits = args.mcmc_iters
         burn = nits // 2
         walk = np.ones(P, np.uint8)
+        eng.mh_run(theta, y0, nits=2, burnin=0, walk_mask=walk, rng="philox", seed=1)  # load the kernel
         torch.cuda.synchronize(dev)
         tm0 = time.perf_counter()
         r = eng.mh_run(theta, y0, nits=nits, burnin=burn, walk_mask=walk, rng="philox", seed=1234,

@@ -95,8 +95,8 @@ typedef struct oe_ctx oe_ctx;
 typedef struct {
   int32_t model_id;          /* OE_MODEL_* */
   int32_t n_states;          /* S (for OE_MODEL_CHAIN: N) */
-  int32_t n_params;          /* P >= model's own parameter count; extra entries are
-                                e.g. '<state>0' initial-condition parameters */
+  int32_t n_params;          /* model's own P <= n_params <= P + min(S, 4); extra entries
+                                are e.g. '<state>0' initial-condition parameters */
   int32_t n_times;           /* T >= 2 */
   const double* times;       /* [T] host, strictly increasing (np.linspace grid) */
   int32_t n_obs;             /* number of observations (0 = no likelihood) */

@@ -196,8 +196,9 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
                                            " with S=" + std::to_string(p->n_states) +
                                            " is not compiled in");
   if (p->n_states != e->S) return fail(c, OE_ERR_ARG, "oe_problem_set: n_states mismatch");
-  if (p->n_params < e->P || p->n_params > e->P + e->S || p->n_params > 64)
-    return fail(c, OE_ERR_ARG, "oe_problem_set: n_params must be in [model P, model P + S]");
+  const int pmax = e->P + (e->S < 4 ? e->S : 4);  // kPmax<M>
+  if (p->n_params < e->P || p->n_params > pmax)
+    return fail(c, OE_ERR_ARG, "oe_problem_set: n_params must be in [model P, model P + min(S, 4)]");
   if (p->n_times < 2 || !p->times) return fail(c, OE_ERR_ARG, "oe_problem_set: need >= 2 times");
   for (int i = 1; i < p->n_times; ++i)
     if (!(p->times[i] > p->times[i - 1]))

@@ -47,7 +47,7 @@ struct DevProblem {
   const Obs* obs;       // [n_obs]
   int32_t T;
   int32_t n_obs;
-  int32_t P;            // runtime parameter count (<= Model::P + Model::S)
+  int32_t P;            // runtime parameter count (<= kPmax<Model>)
   int32_t substeps;     // RK4 steps per output interval
   double rtol, atol;
   int32_t max_steps;    // DOPRI5 steps per output interval
@@ -76,15 +76,39 @@ __device__ __forceinline__ int32_t finish(const Acc& a) {
   return st;
 }
 
+// Cross-lane max/min of a double over the 64-lane wave with DPP row operations
+// (quad_perm xor1/xor2, row_half_mirror, row_mirror, row_bcast15, row_bcast31), then
+// v_readlane of lane 63: ~18 VALU ops and no LDS round trip (ds_bpermute costs a lone
+// wave ~60+ cycles per hop).  Result is wave-uniform.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xF, false);
+  const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xF, false);
+  return __hiloint2double(hi2, lo2);
+}
+__device__ __forceinline__ double lane63(double v) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-  return v;
+  v = fmax(v, dpp_f64<0xB1>(v));        // quad_perm [1,0,3,2]
+  v = fmax(v, dpp_f64<0x4E>(v));        // quad_perm [2,3,0,1]
+  v = fmax(v, dpp_f64<0x141>(v));       // row_half_mirror
+  v = fmax(v, dpp_f64<0x140>(v));       // row_mirror
+  v = fmax(v, dpp_f64<0x142, 0xA>(v));  // row_bcast15 -> rows 1, 3
+  v = fmax(v, dpp_f64<0x143, 0xC>(v));  // row_bcast31 -> rows 2, 3
+  return lane63(v);
 }
 __device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
-  return v;
+  v = fmin(v, dpp_f64<0xB1>(v));
+  v = fmin(v, dpp_f64<0x4E>(v));
+  v = fmin(v, dpp_f64<0x141>(v));
+  v = fmin(v, dpp_f64<0x140>(v));
+  v = fmin(v, dpp_f64<0x142, 0xA>(v));
+  v = fmin(v, dpp_f64<0x143, 0xC>(v));
+  return lane63(v);
 }
 
 // register-array element at a (uniform) runtime index without spilling the array
@@ -316,44 +340,61 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
   while (i < pb.T) {
     bool last = false;
     if (t + h >= tend) { h = tend - t; last = true; }
-    // ---- stages ----
+    // h-scaled tableau (wave-uniform), then one fma chain per stage and state
+    const double b21 = h * a21;
+    const double b31 = h * a31, b32 = h * a32;
+    const double b41 = h * a41, b42 = h * a42, b43 = h * a43;
+    const double b51 = h * a51, b52 = h * a52, b53 = h * a53, b54 = h * a54;
+    const double b61 = h * a61, b62 = h * a62, b63 = h * a63, b64 = h * a64, b65 = h * a65;
+    const double b71 = h * a71, b73 = h * a73, b74 = h * a74, b75 = h * a75, b76 = h * a76;
 #pragma unroll
-    for (int s = 0; s < S; ++s) yt[s] = y[s] + h * (a21 * k1[s]);
+    for (int s = 0; s < S; ++s) yt[s] = fma(b21, k1[s], y[s]);
     M::rhs(yt, t + c2 * h, p, k2);
 #pragma unroll
-    for (int s = 0; s < S; ++s) yt[s] = y[s] + h * (a31 * k1[s] + a32 * k2[s]);
+    for (int s = 0; s < S; ++s) yt[s] = fma(b32, k2[s], fma(b31, k1[s], y[s]));
     M::rhs(yt, t + c3 * h, p, k3);
 #pragma unroll
-    for (int s = 0; s < S; ++s) yt[s] = y[s] + h * (a41 * k1[s] + a42 * k2[s] + a43 * k3[s]);
+    for (int s = 0; s < S; ++s) yt[s] = fma(b43, k3[s], fma(b42, k2[s], fma(b41, k1[s], y[s])));
     M::rhs(yt, t + c4 * h, p, k4);
 #pragma unroll
     for (int s = 0; s < S; ++s)
-      yt[s] = y[s] + h * (a51 * k1[s] + a52 * k2[s] + a53 * k3[s] + a54 * k4[s]);
+      yt[s] = fma(b54, k4[s], fma(b53, k3[s], fma(b52, k2[s], fma(b51, k1[s], y[s]))));
     M::rhs(yt, t + c5 * h, p, k5);
 #pragma unroll
     for (int s = 0; s < S; ++s)
-      yt[s] = y[s] + h * (a61 * k1[s] + a62 * k2[s] + a63 * k3[s] + a64 * k4[s] + a65 * k5[s]);
+      yt[s] = fma(b65, k5[s], fma(b64, k4[s], fma(b63, k3[s], fma(b62, k2[s], fma(b61, k1[s], y[s])))));
     M::rhs(yt, t + h, p, k6);
 #pragma unroll
     for (int s = 0; s < S; ++s)
-      yn[s] = y[s] + h * (a71 * k1[s] + a73 * k3[s] + a74 * k4[s] + a75 * k5[s] + a76 * k6[s]);
+      yn[s] = fma(b76, k6[s], fma(b75, k5[s], fma(b74, k4[s], fma(b73, k3[s], fma(b71, k1[s], y[s])))));
     M::rhs(yn, t + h, p, k7);
-    // ---- per-lane max-norm error, wave max ----
-    double el = 0.0;
+    // ---- per-lane max-norm error: argmax of |e_s|/sk_s by exact cross-multiplication,
+    //      then ONE division; non-finite anywhere -> 1e30 (forces a reject) ----
+    const double g1 = h * e1, g3 = h * e3, g4 = h * e4, g5 = h * e5, g6 = h * e6, g7 = h * e7;
+    double num = 0.0, den = 1.0, nfe = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const double e = h * (e1 * k1[s] + e3 * k3[s] + e4 * k4[s] + e5 * k5[s] + e6 * k6[s] + e7 * k7[s]);
-      const double sk = atol + rtol * fmax(fabs(y[s]), fabs(yn[s]));
-      el = fmax(el, fabs(e) / sk);
+      const double e = fma(g7, k7[s], fma(g6, k6[s], fma(g5, k5[s], fma(g4, k4[s], fma(g3, k3[s], g1 * k1[s])))));
+      const double ae = fabs(e);
+      const double sk = fma(rtol, fmax(fabs(y[s]), fabs(yn[s])), atol);
+      nfe = fma(ae, 0.0, nfe);
+      if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
     }
-    if (!__builtin_isfinite(el)) el = 1e30;  // also catches NaN (fmax would drop it)
+    double el = num / den;
+    if (!__builtin_isfinite(el) || __builtin_isnan(nfe)) el = 1e30;
     if (dead) el = 0.0;
     const double err = wave_max(el);
     ++nst;
 
     if (err <= 1.0) {
       const double tn = last ? tend : t + h;
-      // dense output for every grid point in (t, tn]
+      // dense output for every grid point in (t, tn]; for small S Hairer's coefficients
+      // are formed once per step (on the first grid point that needs them), for large S
+      // per grid point (four more S-vectors would spill)
+      constexpr bool kHoist = S <= 8;
+      bool have_dense = false;
+      double ydf[kHoist ? S : 1], bsp[kHoist ? S : 1], r4[kHoist ? S : 1], r5[kHoist ? S : 1];
+      const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
       while (i < pb.T && times[i] <= tn) {
         if (grid_needs_emit<S, TRAJ>(pb, i, k)) {
           double yo[S];
@@ -364,14 +405,29 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
           } else {
             const double th = (ti - t) / h;
             const double th1 = 1.0 - th;
+            if constexpr (kHoist) {
+              if (!have_dense) {
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-              const double ydiff = yn[s] - y[s];
-              const double bspl = h * k1[s] - ydiff;
-              const double r4 = ydiff - h * k7[s] - bspl;
-              const double r5 = h * (d1 * k1[s] + d3 * k3[s] + d4 * k4[s] + d5 * k5[s] +
-                                     d6 * k6[s] + d7 * k7[s]);
-              yo[s] = y[s] + th * (ydiff + th1 * (bspl + th * (r4 + th1 * r5)));
+                for (int s = 0; s < S; ++s) {
+                  ydf[s] = yn[s] - y[s];
+                  bsp[s] = fma(h, k1[s], -ydf[s]);
+                  r4[s] = fma(-h, k7[s], ydf[s]) - bsp[s];
+                  r5[s] = fma(hd7, k7[s], fma(hd6, k6[s], fma(hd5, k5[s], fma(hd4, k4[s], fma(hd3, k3[s], hd1 * k1[s])))));
+                }
+                have_dense = true;
+              }
+#pragma unroll
+              for (int s = 0; s < S; ++s)
+                yo[s] = fma(th, fma(th1, fma(th, fma(th1, r5[s], r4[s]), bsp[s]), ydf[s]), y[s]);
+            } else {
+#pragma unroll
+              for (int s = 0; s < S; ++s) {
+                const double ydf1 = yn[s] - y[s];
+                const double bsp1 = fma(h, k1[s], -ydf1);
+                const double r41 = fma(-h, k7[s], ydf1) - bsp1;
+                const double r51 = fma(hd7, k7[s], fma(hd6, k6[s], fma(hd5, k5[s], fma(hd4, k4[s], fma(hd3, k3[s], hd1 * k1[s])))));
+                yo[s] = fma(th, fma(th1, fma(th, fma(th1, r51, r41), bsp1), ydf1), y[s]);
+              }
             }
           }
           if (dead) {
@@ -386,21 +442,20 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
       for (int s = 0; s < S; ++s) { y[s] = yn[s]; k1[s] = k7[s]; }
       t = tn;
-      double fac = (err > 0.0) ? safe * pow(err, -0.2) : facmax;
+      double fac = (err > 0.0) ? safe * exp(-0.2 * log(err)) : facmax;
       fac = fmin(facmax, fmax(facmin, fac));
       if (last_rej) fac = fmin(fac, 1.0);
       h = h * fac;
       last_rej = false;
     } else {
-      h = h * fmax(facmin, safe * pow(err, -0.2));
+      h = h * fmax(facmin, safe * exp(-0.2 * log(err)));
       last_rej = true;
     }
     // ---- budget: evict the walkers that pin the wave's step ----
     if (nst >= pb.max_steps || h < hmin) {
       if (!dead && el >= 0.5 * err) { dead = true; a.status |= ST_MAXSTEP; }
       nst = pb.max_steps / 2;
-      const double alive = wave_max(dead ? 0.0 : 1.0);
-      if (alive == 0.0) {
+      if (__ballot(!dead) == 0ull) {
         // every lane is out: emit NaN rows for the rest of the grid and stop
         double yo[S];
 #pragma unroll
@@ -438,10 +493,15 @@ struct IntegrateArgs {
   int32_t* status;      // [W] or null
 };
 
+// parameter registers: the model's own P plus up to 4 '<state>0' initial-condition
+// parameters (oe_problem_set enforces n_params <= kPmax<M>)
+template <class M>
+constexpr int kPmax = M::P + (M::S < 4 ? M::S : 4);
+
 template <class M, int METHOD, bool TRAJ, bool NT>
 __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const IntegrateArgs ia) {
   constexpr int S = M::S;
-  constexpr int PMAX = M::P + M::S;
+  constexpr int PMAX = kPmax<M>;
   const int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = gw < ia.W;
   const int64_t w = active ? gw : ia.W - 1;  // tail lanes shadow the last walker, never store
@@ -512,7 +572,7 @@ struct MHArgs {
 template <class M, int METHOD>
 __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma) {
   constexpr int S = M::S;
-  constexpr int PMAX = M::P + M::S;
+  constexpr int PMAX = kPmax<M>;
   const int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = gw < ma.W;
   const int64_t w = active ? gw : ma.W - 1;

@@ -68,9 +68,9 @@ CHAIN_SIZES = (4, 5, 6, 8, 10, 12, 16, 20, 24, 32)  # compiled chain instantiati
 def candidates(n_states: int, n_params: int):
     out = []
     for name, (mid, S, P, f) in BUILTIN.items():
-        if S == n_states and P <= n_params <= P + S:
+        if S == n_states and P <= n_params <= P + min(S, 4):
             out.append((name, mid, S, P, f))
-    if n_states in CHAIN_SIZES and 5 <= n_params <= 5 + n_states:
+    if n_states in CHAIN_SIZES and 5 <= n_params <= 5 + min(n_states, 4):
         out.append(("chain", N.OE_MODEL_CHAIN, n_states, 5, chain_rhs(n_states)))
     return out
 

@@ -242,31 +242,43 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
   while (i < pb->T) {
     int last = 0;
     if (t + h >= tend) { h = tend - t; last = 1; }
+    /* h-scaled tableau, one fma chain per stage and state */
+    const double b21 = h * a21;
+    const double b31 = h * a31, b32 = h * a32;
+    const double b41 = h * a41, b42 = h * a42, b43 = h * a43;
+    const double b51 = h * a51, b52 = h * a52, b53 = h * a53, b54 = h * a54;
+    const double b61 = h * a61, b62 = h * a62, b63 = h * a63, b64 = h * a64, b65 = h * a65;
+    const double b71 = h * a71, b73 = h * a73, b74 = h * a74, b75 = h * a75, b76 = h * a76;
+    const double g1 = h * e1, g3 = h * e3, g4 = h * e4, g5 = h * e5, g6 = h * e6, g7 = h * e7;
     for (int l = 0; l < nl; ++l) {
       Lane* q = &L[l];
       const double* pl = p + l * MAXP;
-      for (int s = 0; s < S; ++s) q->yt[s] = q->y[s] + h * (a21 * q->k1[s]);
+      for (int s = 0; s < S; ++s) q->yt[s] = fma(b21, q->k1[s], q->y[s]);
       rhs(pb, q->yt, t + c2 * h, pl, q->k2);
-      for (int s = 0; s < S; ++s) q->yt[s] = q->y[s] + h * (a31 * q->k1[s] + a32 * q->k2[s]);
+      for (int s = 0; s < S; ++s) q->yt[s] = fma(b32, q->k2[s], fma(b31, q->k1[s], q->y[s]));
       rhs(pb, q->yt, t + c3 * h, pl, q->k3);
-      for (int s = 0; s < S; ++s) q->yt[s] = q->y[s] + h * (a41 * q->k1[s] + a42 * q->k2[s] + a43 * q->k3[s]);
+      for (int s = 0; s < S; ++s) q->yt[s] = fma(b43, q->k3[s], fma(b42, q->k2[s], fma(b41, q->k1[s], q->y[s])));
       rhs(pb, q->yt, t + c4 * h, pl, q->k4);
       for (int s = 0; s < S; ++s)
-        q->yt[s] = q->y[s] + h * (a51 * q->k1[s] + a52 * q->k2[s] + a53 * q->k3[s] + a54 * q->k4[s]);
+        q->yt[s] = fma(b54, q->k4[s], fma(b53, q->k3[s], fma(b52, q->k2[s], fma(b51, q->k1[s], q->y[s]))));
       rhs(pb, q->yt, t + c5 * h, pl, q->k5);
       for (int s = 0; s < S; ++s)
-        q->yt[s] = q->y[s] + h * (a61 * q->k1[s] + a62 * q->k2[s] + a63 * q->k3[s] + a64 * q->k4[s] + a65 * q->k5[s]);
+        q->yt[s] = fma(b65, q->k5[s], fma(b64, q->k4[s], fma(b63, q->k3[s], fma(b62, q->k2[s], fma(b61, q->k1[s], q->y[s])))));
       rhs(pb, q->yt, t + h, pl, q->k6);
       for (int s = 0; s < S; ++s)
-        q->yn[s] = q->y[s] + h * (a71 * q->k1[s] + a73 * q->k3[s] + a74 * q->k4[s] + a75 * q->k5[s] + a76 * q->k6[s]);
+        q->yn[s] = fma(b76, q->k6[s], fma(b75, q->k5[s], fma(b74, q->k4[s], fma(b73, q->k3[s], fma(b71, q->k1[s], q->y[s])))));
       rhs(pb, q->yn, t + h, pl, q->k7);
-      double el = 0.0;
+      /* argmax of |e|/sk by exact cross-multiplication, then one division */
+      double num = 0.0, den = 1.0, nfe = 0.0;
       for (int s = 0; s < S; ++s) {
-        double e = h * (e1 * q->k1[s] + e3 * q->k3[s] + e4 * q->k4[s] + e5 * q->k5[s] + e6 * q->k6[s] + e7 * q->k7[s]);
-        double sk = atol + rtol * fmax(fabs(q->y[s]), fabs(q->yn[s]));
-        el = fmax(el, fabs(e) / sk);
+        double e = fma(g7, q->k7[s], fma(g6, q->k6[s], fma(g5, q->k5[s], fma(g4, q->k4[s], fma(g3, q->k3[s], g1 * q->k1[s])))));
+        double ae = fabs(e);
+        double sk = fma(rtol, fmax(fabs(q->y[s]), fabs(q->yn[s])), atol);
+        nfe = fma(ae, 0.0, nfe);
+        if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
       }
-      if (!isfinite(el)) el = 1e30;
+      double el = num / den;
+      if (!isfinite(el) || isnan(nfe)) el = 1e30;
       if (q->dead) el = 0.0;
       q->el = el;
     }
@@ -274,6 +286,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     ++nst;
     if (err <= 1.0) {
       double tn = last ? tend : t + h;
+      const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
       while (i < pb->T && pb->times[i] <= tn) {
         for (int l = 0; l < nl; ++l) {
           Lane* q = &L[l];
@@ -285,11 +298,11 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
           } else {
             double th = (ti - t) / h, th1 = 1.0 - th;
             for (int s = 0; s < S; ++s) {
-              double ydiff = q->yn[s] - q->y[s];
-              double bspl = h * q->k1[s] - ydiff;
-              double r4 = ydiff - h * q->k7[s] - bspl;
-              double r5 = h * (d1 * q->k1[s] + d3 * q->k3[s] + d4 * q->k4[s] + d5 * q->k5[s] + d6 * q->k6[s] + d7 * q->k7[s]);
-              yo[s] = q->y[s] + th * (ydiff + th1 * (bspl + th * (r4 + th1 * r5)));
+              double ydf = q->yn[s] - q->y[s];
+              double bsp = fma(h, q->k1[s], -ydf);
+              double r4 = fma(-h, q->k7[s], ydf) - bsp;
+              double r5 = fma(hd7, q->k7[s], fma(hd6, q->k6[s], fma(hd5, q->k5[s], fma(hd4, q->k4[s], fma(hd3, q->k3[s], hd1 * q->k1[s])))));
+              yo[s] = fma(th, fma(th1, fma(th, fma(th1, r5, r4), bsp), ydf), q->y[s]);
             }
           }
           if (q->dead)
@@ -304,13 +317,13 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
         memcpy(L[l].k1, L[l].k7, sizeof(double) * S);
       }
       t = tn;
-      double fac = (err > 0.0) ? 0.9 * pow(err, -0.2) : 10.0;
+      double fac = (err > 0.0) ? 0.9 * exp(-0.2 * log(err)) : 10.0;
       fac = fmin(10.0, fmax(0.2, fac));
       if (last_rej) fac = fmin(fac, 1.0);
       h = h * fac;
       last_rej = 0;
     } else {
-      h = h * fmax(0.2, 0.9 * pow(err, -0.2));
+      h = h * fmax(0.2, 0.9 * exp(-0.2 * log(err)));
       last_rej = 1;
     }
     if (nst >= pb->max_steps || h < hmin) {

@@ -57,6 +57,44 @@ __global__ void __launch_bounds__(256) store_kernel(double* out, long W, int T, 
   }
 }
 
+// L3: [T][S][W] through a per-row buffer descriptor (the engine's current store path),
+// cache-policy bits `AUX` (gfx950 aux: sc0=1, nt=2, sc1=16)
+template <int AUX, int S>
+__global__ void __launch_bounds__(256) buf_kernel(double* out, long W, int T, int work, double a) {
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  const long gw = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gw >= W) return;
+  double y[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) y[s] = 1.0 + 1e-3 * s + 1e-9 * (double)gw;
+  const unsigned off = (unsigned)gw * 8u;
+  for (int t = 0; t < T; ++t) {
+    for (int k = 0; k < work; ++k) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) y[s] = fma(y[s], a, 1e-7);
+    }
+    auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(out + (long)t * S * W), 0, (unsigned)(S * W * 8), 0x00020000);
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, y[s]), rsrc, off, (unsigned)(s * W * 8), AUX);
+  }
+}
+
+template <int AUX>
+float runbuf(double* out, long W, int T, int work, int reps) {
+  dim3 g((unsigned)((W + 255) / 256)), b(256);
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((buf_kernel<AUX, 4>), g, b, 0, 0, out, W, T, work, 0.999999);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((buf_kernel<AUX, 4>), g, b, 0, 0, out, W, T, work, 0.999999);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+
 template <int LAYOUT, bool NT>
 float run(double* out, long W, int T, int work, int reps) {
   constexpr int S = 4;
@@ -89,6 +127,15 @@ int main(int argc, char** argv) {
     printf("work=%2d fma/step/state | L0 %.3f ms %.2f TB/s | L0nt %.3f %.2f | L1 %.3f %.2f | L1nt %.3f %.2f | "
            "L2 %.3f %.2f | L2nt %.3f %.2f\n",
            work, t00, bw(t00), t01, bw(t01), t10, bw(t10), t11, bw(t11), t20, bw(t20), t21, bw(t21));
+  }
+  for (int work : {0, 14}) {
+    auto bw = [&](float ms) { return bytes / (ms * 1e-3) / 1e12; };
+    float a0 = runbuf<0>(out, W, T, work, reps), a1 = runbuf<1>(out, W, T, work, reps), a2 = runbuf<2>(out, W, T, work, reps);
+    float a3 = runbuf<3>(out, W, T, work, reps), a16 = runbuf<16>(out, W, T, work, reps), a17 = runbuf<17>(out, W, T, work, reps);
+    float a18 = runbuf<18>(out, W, T, work, reps), a19 = runbuf<19>(out, W, T, work, reps);
+    printf("buffer work=%2d | aux0 %.3f ms %.2f | aux1 %.3f %.2f | aux2(nt) %.3f %.2f | aux3 %.3f %.2f | aux16 %.3f %.2f | "
+           "aux17 %.3f %.2f | aux18 %.3f %.2f | aux19 %.3f %.2f TB/s\n", work, a0, bw(a0), a1, bw(a1), a2, bw(a2), a3, bw(a3),
+           a16, bw(a16), a17, bw(a17), a18, bw(a18), a19, bw(a19));
   }
   CHECK(hipFree(out));
   return 0;
