@@ -80,7 +80,8 @@ enum {
 enum {
   OE_HOST_PTRS = 1u, /* buffers are host memory */
   OE_ASYNC = 2u,     /* do not synchronize before returning (device pointers only) */
-  OE_NT_STORES = 4u  /* non-temporal trajectory stores */
+  OE_NT_STORES = 4u, /* non-temporal trajectory stores */
+  OE_PIPE = 8u       /* RK4 trajectories via the producer/consumer kernel (opt-in, S <= 8, W even) */
 };
 
 /* RNG modes for oe_mh_run */

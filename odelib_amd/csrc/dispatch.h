@@ -17,12 +17,17 @@ struct Entry {
   int32_t P;  // the model's own parameter count
   // [method][traj][nt]
   IntegrateLaunch integrate[2][2][2];
+  IntegrateLaunch rk4_piped[2];  // [nt]; null when S > 8 (LDS ring too large)
   MHLaunch mh[2];
 };
 
 template <class M, int METHOD, bool TRAJ, bool NT>
 void launch_integrate(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_integrate<M, METHOD, TRAJ, NT>), g, b, 0, s, pb, ia);
+}
+template <class M, bool NT>
+void launch_rk4_piped(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_integrate_rk4_piped<M, NT>), g, b, 0, s, pb, ia);
 }
 template <class M, int METHOD>
 void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
@@ -43,6 +48,10 @@ Entry make_entry(int32_t model_id) {
   e.integrate[1][1][0] = launch_integrate<M, 1, true, false>;
   e.integrate[1][1][1] = launch_integrate<M, 1, true, true>;
   e.integrate[1][0][1] = launch_integrate<M, 1, false, false>;
+  if constexpr (M::S <= 8) {
+    e.rk4_piped[0] = launch_rk4_piped<M, false>;
+    e.rk4_piped[1] = launch_rk4_piped<M, true>;
+  }
   e.mh[0] = launch_mh<M, 0>;
   e.mh[1] = launch_mh<M, 1>;
   return e;

@@ -521,6 +521,137 @@ __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const In
 }
 
 // ---------------------------------------------------------------------------------
+// Kernel 1b: RK4 trajectory mode with producer/consumer waves (S <= 8, W even).
+//
+// One 384-thread workgroup = 4 COMPUTE waves (256 walkers, one per lane) + 2 STORE
+// waves.  Output rows are produced in phases of H rows into one half of a
+// double-buffered LDS ring [2][H][S][256]; in the next phase the store waves read that
+// half with ds_read_b128 (two consecutive walkers per lane) and write 1 KB per
+// wave-instruction with buffer_store_dwordx4, while the compute waves fill the other
+// half.  Phases are separated by a raw s_barrier behind an lgkmcnt(0) wait only, so
+// the global stores stay in flight across barriers and the compute waves never wait on
+// vmcnt.  Same arithmetic, same outputs as k_integrate<M, RK4, true, NT>.
+// ---------------------------------------------------------------------------------
+constexpr int kPipeWalkers = 256;  // walkers per workgroup (4 compute waves)
+constexpr int kPipeThreads = 384;  // + 2 store waves
+constexpr int kPipeLdsBytes = 128 * 1024;
+
+template <int S>
+constexpr int pipe_rows() { return (kPipeLdsBytes / (2 * S * kPipeWalkers * 8)) > 0 ? (kPipeLdsBytes / (2 * S * kPipeWalkers * 8)) : 1; }
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <class M, bool NT>
+__global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevProblem pb, const IntegrateArgs ia) {
+  constexpr int S = M::S;
+  constexpr int PMAX = kPmax<M>;
+  constexpr int H = pipe_rows<S>();
+  static_assert(2 * H * S * kPipeWalkers * 8 <= kPipeLdsBytes, "LDS ring too large");
+  __shared__ double ring[2][H][S][kPipeWalkers];
+
+  const int64_t W = ia.W;
+  const int T = pb.T;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t base = (int64_t)blockIdx.x * kPipeWalkers;
+  const int nphase = (T + H - 1) / H;
+
+  if (wave < 4) {
+    // ------------------------------ compute waves ------------------------------
+    const int b = wave * 64 + lane;  // walker slot in the block
+    const int64_t gw = base + b;
+    const bool active = gw < W;
+    const int64_t w = active ? gw : W - 1;
+    double y[S], p[PMAX];
+#pragma unroll
+    for (int s = 0; s < S; ++s) y[s] = ia.y0[(int64_t)s * W + w];
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
+    Acc a = acc_init();
+    int k = 0;
+    const cptr<double> tab = kconst(pb.rk4);
+    const cptr<Obs> obs = kconst(pb.obs);
+    const int n = pb.substeps;
+    auto put = [&](int half, int h, const double (&v)[S]) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) ring[half][h][s][b] = v[s];
+#pragma unroll
+      for (int s = 0; s < S; ++s) a.ymin = fmin(a.ymin, v[s]);
+    };
+    auto interval = [&](int i) {
+      const double h = tab[4 * (i - 1)], hh = tab[4 * (i - 1) + 1], h6 = tab[4 * (i - 1) + 2];
+      const double t = tab[4 * (i - 1) + 3];
+      for (int j = 0; j < n; ++j) rk4_step<M, PMAX>(y, t + (double)j * h, h, hh, h6, p);
+    };
+    for (int ph = 0; ph <= nphase; ++ph) {
+      if (ph < nphase) {
+        const int half = ph & 1;
+        const int r0 = ph * H;
+        const int r1 = (r0 + H < T) ? r0 + H : T;
+        int r = r0;
+        if (r == 0) {  // row 0 is the initial state
+          put(half, 0, y);
+          observe<S>(pb, 0, y, k, a);
+          ++r;
+        }
+        while (r < r1) {
+          int next = (k < pb.n_obs) ? obs[k].tidx : T;
+          if (next > r1) next = r1;
+          for (; r < next; ++r) {
+            interval(r);
+            put(half, r - r0, y);
+          }
+          if (r < r1) {  // observed row
+            interval(r);
+            put(half, r - r0, y);
+            observe<S>(pb, r, y, k, a);
+            ++r;
+          }
+        }
+      }
+      lds_barrier();
+    }
+    check_finite(y, a);
+    if (active) {
+      if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
+      if (ia.ssres) ia.ssres[w] = a.ssres;
+      if (ia.status) ia.status[w] = finish(a);
+    }
+  } else {
+    // ------------------------------ store waves --------------------------------
+    const int sw = wave - 4;                 // 0 or 1: walkers [128*sw, 128*sw + 128)
+    const int b = sw * 128 + 2 * lane;       // first of this lane's two walkers
+    const bool active = base + b < W;        // W even: both or neither
+    const uint32_t off = (uint32_t)(base + b) * 8u;
+    const uint32_t row_bytes = (uint32_t)(S * W * 8);
+    for (int ph = 0; ph <= nphase; ++ph) {
+      if (ph >= 1) {
+        const int half = (ph - 1) & 1;
+        const int r0 = (ph - 1) * H;
+        const int r1 = (r0 + H < T) ? r0 + H : T;
+        for (int r = r0; r < r1; ++r) {
+          const __amdgpu_buffer_rsrc_t rsrc =
+              __builtin_amdgcn_make_buffer_rsrc((void*)(ia.traj + (int64_t)r * S * W), 0, row_bytes, 0x00020000);
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(&ring[half][r - r0][s][b]);
+            if (active)
+              __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, (uint32_t)(s * W * 8), NT ? 2 : 0);
+          }
+        }
+      }
+      lds_barrier();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11) counter-based RNG for the MH proposals.
 // ---------------------------------------------------------------------------------
 struct U4 { uint32_t x, y, z, w; };

@@ -61,6 +61,24 @@ def test_rk4_bitwise_vs_c_restatement(spec, W):
     assert np.array_equal(out["status"], ref["status"])
 
 
+@pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain5", "chain8"])
+@pytest.mark.parametrize("W", [2, 258, 4098])
+def test_rk4_pipelined_kernel_matches_direct_kernel(spec, W):
+    """The producer/consumer trajectory kernel (4 compute + 2 store waves, LDS ring)
+    gives the same bits as the one-lane-per-walker kernel, incl. ragged tail blocks."""
+    m = _model(spec, "rk4")
+    theta = _walkers(spec, W)
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    eng = m.engine()
+    a = eng.integrate(y0, theta, pipelined=True)
+    b = eng.integrate(y0, theta, pipelined=False)
+    for key in ("traj", "chi", "ssres", "status"):
+        assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
+    for nt in (False, True):
+        c = eng.integrate(y0, theta, pipelined=True, nt_stores=nt)
+        assert np.array_equal(c["traj"].cpu().numpy(), b["traj"].cpu().numpy())
+
+
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain8"])
 def test_rk4_substeps_bitwise(spec):
     m = _model(spec, "rk4", substeps=3)
