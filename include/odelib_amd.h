@@ -66,7 +66,8 @@ enum {
   OE_MODEL_ZERO_I = 0, /* S=2 (S,V),        P=3 (mu,phi,beta)         notebook zero_i */
   OE_MODEL_ONE_I = 1,  /* S=3 (S,I1,V),     P=4 (mu,phi,beta,lam)     notebook one_i  */
   OE_MODEL_TWO_I = 2,  /* S=4 (S,I1,I2,V),  P=5 (mu,phi,beta,lam,tau) notebook two_i  */
-  OE_MODEL_CHAIN = 3   /* S=N (S,I1..I_{N-2},V), P=5; N=4 reduces to two_i */
+  OE_MODEL_CHAIN = 3,  /* S=N (S,I1..I_{N-2},V), P=5; N=4 reduces to two_i */
+  OE_MODEL_CUSTOM = 1000 /* first id handed out by oe_model_compile (per context) */
 };
 
 /* per-walker status bits (OR-ed) */
@@ -144,6 +145,18 @@ int oe_abi_version(void);
 /* Model registry query: fills S (for CHAIN pass the wanted N in *n_states) and the
  * model's own parameter count.  Returns OE_ERR_UNSUPPORTED if not compiled in. */
 int oe_model_info(int32_t model_id, int32_t* n_states, int32_t* n_params);
+
+/* User right-hand side compiled at run time (hipRTC) for this context's device.
+ * rhs_body is the body of
+ *     template <class R> __device__ void rhs(const R* y, R t, const R* ps, R* dy)
+ * (C++; y[0..n_states), ps[0..n_params), t; must assign dy[0..n_states)), i.e. the
+ * reference's ODE(y, t, ps) callable (Framework.py:177-180) re-declared in C.  On success
+ * *model_id (>= OE_MODEL_CUSTOM) is usable in oe_problem.model_id with this context.
+ * Compile errors are returned as OE_ERR_ARG with the compiler log in oe_last_error. */
+int oe_model_compile(oe_ctx* ctx, const char* rhs_body, int32_t n_states, int32_t n_params, int32_t* model_id);
+/* Compile-only check of a user RHS for target `arch` (e.g. "gfx950"); needs no GPU.
+ * Errors: oe_last_error(NULL). */
+int oe_rtc_check(const char* rhs_body, int32_t n_states, int32_t n_params, const char* arch);
 
 int oe_ctx_create(int32_t device, oe_ctx** out);
 void oe_ctx_destroy(oe_ctx* ctx);

@@ -8,7 +8,9 @@ ODE callable is bound to a compiled device RHS by ``models.resolve``.
 
 Engine options (keyword-only, new): ``method`` ('dopri5' default — adaptive like
 odeint — or 'rk4'), ``rtol``/``atol`` (odeint defaults), ``rk4_substeps``,
-``max_steps`` (odeint's mxstep), ``device`` (HIP device index), ``device_model``.
+``max_steps`` (odeint's mxstep), ``device`` (HIP device index), ``device_model``
+(force a built-in RHS, or 'rtc'), ``device_rhs`` (C++ body of the RHS for hipRTC).
+An ODE callable that matches no built-in is transpiled to C and compiled at run time.
 ``MCMC`` runs every chain as one walker of a single batched launch; ``rng='replay'``
 (default) reproduces the reference's numpy draws per chain, ``rng='philox'`` draws
 on device for large ensembles.
@@ -26,7 +28,7 @@ from .Statistics import Samplers, stats
 from .engine import ODEINT_TOL, Engine, FitProblem
 from .rng import legacy_replay_streams
 
-_ENGINE_KW = ("method", "rtol", "atol", "rk4_substeps", "max_steps", "device", "device_model")
+_ENGINE_KW = ("method", "rtol", "atol", "rk4_substeps", "max_steps", "device", "device_model", "device_rhs")
 
 
 def rawstats(pdseries):
@@ -119,6 +121,7 @@ class ModelFramework:
         self.max_steps = int(eng.get("max_steps", 500))
         self.device = int(eng.get("device", 0))
         self.device_model = eng.get("device_model", None)
+        self.device_rhs = eng.get("device_rhs", None)
         self._engine = None
         self._engine_key = None
 
@@ -331,7 +334,9 @@ class ModelFramework:
 
     def fit_problem(self) -> FitProblem:
         """Constant kernel inputs."""
-        mid, S = _models.resolve(self._model, len(self._snames), len(self._pnames), self.device_model)
+        dm = _models.resolve_model(self._model, len(self._snames), len(self._pnames), self.device_model,
+                                   self.device_rhs)
+        mid, S = (dm.model_id if dm.model_id is not None else -1), dm.n_states
         _, cols, keep = self._obs_layout()
         tidx, mask, O, Ssig, lin = [], [], [], [], []
         sstot = 0
@@ -355,11 +360,11 @@ class ModelFramework:
                           obs_logsigma=cat(Ssig, float), obs_lin=cat(lin, float),
                           sstot=float(sstot) if cols else 1.0, pnum=int(self._pnum), method=self.method,
                           rk4_substeps=self.rk4_substeps, rtol=self.rtol, atol=self.atol,
-                          max_steps=self.max_steps)
+                          max_steps=self.max_steps, custom_source=dm.source)
 
     def engine(self) -> Engine:
         key = (self.method, self.rtol, self.atol, self.rk4_substeps, self.max_steps, self.device,
-               self.device_model, id(self.df), len(self.times), float(self.times[-1]))
+               self.device_model, self.device_rhs, id(self.df), len(self.times), float(self.times[-1]))
         if self._engine is None or self._engine_key != key:
             fp = self.fit_problem()
             if self._engine is None or self._engine.device != self.device:

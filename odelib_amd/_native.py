@@ -19,6 +19,7 @@ OE_ABI_VERSION = 1
 OE_OK = 0
 OE_METHOD_RK4, OE_METHOD_DOPRI5 = 0, 1
 OE_MODEL_ZERO_I, OE_MODEL_ONE_I, OE_MODEL_TWO_I, OE_MODEL_CHAIN = 0, 1, 2, 3
+OE_MODEL_CUSTOM = 1000
 OE_STATUS_NONFINITE, OE_STATUS_NEGATIVE, OE_STATUS_MAXSTEP = 1, 2, 4
 OE_HOST_PTRS, OE_ASYNC, OE_NT_STORES, OE_PIPE = 1, 2, 4, 8
 OE_RNG_REPLAY, OE_RNG_PHILOX = 0, 1
@@ -27,6 +28,8 @@ OE_RNG_REPLAY, OE_RNG_PHILOX = 0, 1
 EXPORTED = (
     "oe_abi_version",
     "oe_model_info",
+    "oe_model_compile",
+    "oe_rtc_check",
     "oe_ctx_create",
     "oe_ctx_destroy",
     "oe_last_error",
@@ -115,6 +118,10 @@ def load_library(path: str | None = None):
         lib.oe_abi_version.argtypes = []
         lib.oe_model_info.restype = C.c_int
         lib.oe_model_info.argtypes = [i32, C.POINTER(i32), C.POINTER(i32)]
+        lib.oe_model_compile.restype = C.c_int
+        lib.oe_model_compile.argtypes = [vp, C.c_char_p, i32, i32, C.POINTER(i32)]
+        lib.oe_rtc_check.restype = C.c_int
+        lib.oe_rtc_check.argtypes = [C.c_char_p, i32, i32, C.c_char_p]
         lib.oe_ctx_create.restype = C.c_int
         lib.oe_ctx_create.argtypes = [i32, C.POINTER(vp)]
         lib.oe_ctx_destroy.restype = None
@@ -149,6 +156,14 @@ def model_info(model_id: int, n_states: int = 0) -> tuple[int, int]:
     return s.value, p.value
 
 
+def rtc_check(rhs_body: str, n_states: int, n_params: int, arch: str = "gfx950"):
+    """Compile-only check of a user RHS body with hipRTC (no GPU needed)."""
+    lib = load_library()
+    rc = lib.oe_rtc_check(rhs_body.encode(), int(n_states), int(n_params), arch.encode())
+    if rc != OE_OK:
+        raise ValueError(lib.oe_last_error(None).decode())
+
+
 class Context:
     """One oe_ctx (device, stream, events, device copy of the problem)."""
 
@@ -175,6 +190,13 @@ class Context:
 
     def use_own_stream(self):
         self._check(self.lib.oe_ctx_use_own_stream(self._h), "oe_ctx_use_own_stream")
+
+    def model_compile(self, rhs_body: str, n_states: int, n_params: int) -> int:
+        """hipRTC-compile a user RHS for this device; returns its model id."""
+        mid = C.c_int32(0)
+        self._check(self.lib.oe_model_compile(self._h, rhs_body.encode(), int(n_states), int(n_params),
+                                              C.byref(mid)), "oe_model_compile")
+        return mid.value
 
     def problem_set(self, prob: OEProblem):
         self._check(self.lib.oe_problem_set(self._h, C.byref(prob)), "oe_problem_set")

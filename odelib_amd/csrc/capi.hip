@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <memory>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -61,7 +62,15 @@ constexpr int64_t kMaxWalkers = int64_t(1) << 29;
 
 }  // namespace
 
+struct CustomModel {
+  Entry entry{};
+  RtcModule rtc;
+  std::string body;
+};
+
 struct oe_ctx {
+  std::vector<std::unique_ptr<CustomModel>> custom;  // user RHS modules (model_id = OE_MODEL_CUSTOM + k)
+  std::string arch;
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
@@ -83,8 +92,11 @@ struct oe_ctx {
 
 namespace {
 
+thread_local std::string g_err;  // errors of context-free calls (oe_rtc_check)
+
 int fail(oe_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
+  else g_err = msg;
   return code;
 }
 
@@ -151,6 +163,12 @@ int oe_ctx_create(int32_t device, oe_ctx** out) {
     return OE_ERR_HIP;
   }
   c->stream = c->own_stream;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+    c->arch = prop.gcnArchName;  // e.g. "gfx950:sramecc+:xnack-"
+  } else {
+    c->arch = "gfx950";
+  }
   *out = c;
   return OE_OK;
 }
@@ -166,12 +184,53 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (auto& m : c->custom)
+      if (m->rtc.mod) (void)hipModuleUnload(m->rtc.mod);
     (void)hipStreamDestroy(c->own_stream);
   }
   delete c;
 }
 
-const char* oe_last_error(const oe_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* oe_last_error(const oe_ctx* c) {
+  if (c) return c->err.c_str();
+  return g_err.empty() ? "null context" : g_err.c_str();
+}
+
+int oe_rtc_check(const char* rhs_body, int32_t n_states, int32_t n_params, const char* arch) {
+  if (!rhs_body || n_states < 1 || n_states > 64 || n_params < 1 || n_params > 60)
+    return fail(nullptr, OE_ERR_ARG, "oe_rtc_check: bad arguments");
+  std::string err;
+  if (rtc_build(rhs_body, n_states, n_params, arch ? arch : "gfx950", nullptr, err))
+    return fail(nullptr, OE_ERR_ARG, err);
+  g_err.clear();
+  return OE_OK;
+}
+
+int oe_model_compile(oe_ctx* c, const char* rhs_body, int32_t n_states, int32_t n_params, int32_t* model_id) {
+  if (!c || !c->own_stream) return OE_ERR_STATE;
+  if (!rhs_body || !model_id || n_states < 1 || n_states > 64 || n_params < 1 || n_params > 60)
+    return fail(c, OE_ERR_ARG, "oe_model_compile: bad arguments");
+  for (size_t k = 0; k < c->custom.size(); ++k) {  // cached
+    const CustomModel& m = *c->custom[k];
+    if (m.body == rhs_body && m.entry.S == n_states && m.entry.P == n_params) {
+      *model_id = OE_MODEL_CUSTOM + (int32_t)k;
+      return OE_OK;
+    }
+  }
+  int rc = set_device(c);
+  if (rc) return rc;
+  auto m = std::make_unique<CustomModel>();
+  std::string err;
+  if (rtc_build(rhs_body, n_states, n_params, c->arch.c_str(), &m->rtc, err)) return fail(c, OE_ERR_ARG, err);
+  m->body = rhs_body;
+  m->entry.model_id = OE_MODEL_CUSTOM + (int32_t)c->custom.size();
+  m->entry.S = n_states;
+  m->entry.P = n_params;
+  m->entry.rtc = &m->rtc;
+  *model_id = m->entry.model_id;
+  c->custom.push_back(std::move(m));
+  return OE_OK;
+}
 
 int oe_ctx_set_stream(oe_ctx* c, void* s) {
   if (!c || !c->own_stream) return OE_ERR_STATE;
@@ -190,7 +249,13 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   if (!p) return fail(c, OE_ERR_ARG, "oe_problem_set: null problem");
   int rc = set_device(c);
   if (rc) return rc;
-  const Entry* e = find_entry(p->model_id, p->n_states);
+  const Entry* e = nullptr;
+  if (p->model_id >= OE_MODEL_CUSTOM) {
+    const size_t k = (size_t)(p->model_id - OE_MODEL_CUSTOM);
+    if (k < c->custom.size()) e = &c->custom[k]->entry;
+  } else {
+    e = find_entry(p->model_id, p->n_states);
+  }
   if (!e)
     return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: model " + std::to_string(p->model_id) +
                                            " with S=" + std::to_string(p->n_states) +
@@ -323,7 +388,7 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   // opt-in producer/consumer RK4 trajectory kernel (16-B stores from dedicated store
   // waves; needs W even).  Measured 0.433 vs 0.420 ms for the direct kernel on C1, so
   // it is not the default.
-  const bool piped = (flags & OE_PIPE) && c->method == OE_METHOD_RK4 && ia.traj && e->rk4_piped[nt ? 1 : 0] &&
+  const bool piped = (flags & OE_PIPE) && !e->rtc && c->method == OE_METHOD_RK4 && ia.traj && e->rk4_piped[nt ? 1 : 0] &&
                      (W % 2 == 0);
   OE_HIP(c, hipEventRecord(c->ev0, c->stream));
   if (piped) {
@@ -331,7 +396,7 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     e->rk4_piped[nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
   } else {
     const dim3 grid((unsigned)((W + kBlock - 1) / kBlock)), block(kBlock);
-    e->integrate[c->method][ia.traj ? 1 : 0][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
+    OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));
   }
   OE_HIP(c, hipGetLastError());
   OE_HIP(c, hipEventRecord(c->ev1, c->stream));
@@ -414,14 +479,12 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   m.init = 1;
   m.it0 = 0;
   m.it1 = 0;
-  e->mh[c->method](c->dp, m, grid, block, c->stream);
-  OE_HIP(c, hipGetLastError());
+  OE_HIP(c, launch_mh_entry(e, c->method, c->dp, m, grid, block, c->stream));
   m.init = 0;
   for (int it0 = 1; it0 < a->nits; it0 += chunk) {
     m.it0 = it0;
     m.it1 = std::min(a->nits, it0 + chunk);
-    e->mh[c->method](c->dp, m, grid, block, c->stream);
-    OE_HIP(c, hipGetLastError());
+    OE_HIP(c, launch_mh_entry(e, c->method, c->dp, m, grid, block, c->stream));
   }
   OE_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;

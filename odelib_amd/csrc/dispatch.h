@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "ode_kernels.cuh"
+#include "rtc.h"
 
 namespace oe {
 
@@ -19,7 +20,32 @@ struct Entry {
   IntegrateLaunch integrate[2][2][2];
   IntegrateLaunch rk4_piped[2];  // [nt]; null when S > 8 (LDS ring too large)
   MHLaunch mh[2];
+  const RtcModule* rtc = nullptr;  // user RHS compiled at run time (launchers above unused)
 };
+
+// launch through the ahead-of-time launcher or the hipRTC module function
+inline hipError_t launch_integrate_entry(const Entry* e, int method, int traj, int nt, const DevProblem& dp,
+                                         const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
+  if (e->rtc) {
+    DevProblem a0 = dp;
+    IntegrateArgs a1 = ia;
+    void* args[] = {(void*)&a0, (void*)&a1};
+    return hipModuleLaunchKernel(e->rtc->integrate[method][traj][nt], g.x, g.y, g.z, b.x, b.y, b.z, 0, s, args, nullptr);
+  }
+  e->integrate[method][traj][nt](dp, ia, g, b, s);
+  return hipGetLastError();
+}
+inline hipError_t launch_mh_entry(const Entry* e, int method, const DevProblem& dp, const MHArgs& ma, dim3 g, dim3 b,
+                                  hipStream_t s) {
+  if (e->rtc) {
+    DevProblem a0 = dp;
+    MHArgs a1 = ma;
+    void* args[] = {(void*)&a0, (void*)&a1};
+    return hipModuleLaunchKernel(e->rtc->mh[method], g.x, g.y, g.z, b.x, b.y, b.z, 0, s, args, nullptr);
+  }
+  e->mh[method](dp, ma, g, b, s);
+  return hipGetLastError();
+}
 
 template <class M, int METHOD, bool TRAJ, bool NT>
 void launch_integrate(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {

@@ -1,0 +1,130 @@
+// rtc.hip — run-time compilation of user right-hand sides (hipRTC).
+//
+// The reference integrates any user Python callable ODE(y, t, ps) (Framework.py:177-180,
+// :656).  Built-in models are compiled ahead of time (models.cuh); any other RHS is
+// given as the body of
+//     template <class R> __device__ void rhs(const R* y, R t, const R* ps, R* dy)
+// (C source, or transpiled from the Python callable by odelib_amd/transpile.py) and the
+// SAME kernel templates (ode_kernels.cuh, embedded at build time) are instantiated for
+// it with hiprtc for the device's gfx950 target, loaded as a module and launched with
+// hipModuleLaunchKernel.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "dispatch.h"
+#include "rtc.h"
+#include "rtc_source.inc"
+
+namespace oe {
+
+static const char* kMethodName[2] = {"0", "1"};
+static const char* kBool[2] = {"false", "true"};
+
+std::string rtc_integrate_name(int method, int traj, int nt) {
+  return std::string("oe::k_integrate<UserModel, ") + kMethodName[method] + ", " + kBool[traj] + ", " + kBool[nt] + ">";
+}
+std::string rtc_mh_name(int method) { return std::string("oe::k_mh<UserModel, ") + kMethodName[method] + ">"; }
+
+std::string rtc_source(const std::string& body, int S, int P) {
+  std::string src;
+  src += "typedef unsigned long long uint64_t; typedef long long int64_t;\n";
+  src += "typedef unsigned int uint32_t; typedef int int32_t;\n";
+  src += kRtcKernelSource;
+  char hdr[256];
+  snprintf(hdr, sizeof(hdr), "\nstruct UserModel {\n  static constexpr int S = %d, P = %d;\n", S, P);
+  src += hdr;
+  src += "  template <class R>\n  __device__ static inline void rhs(const R* y, R t, const R* ps, R* dy) {\n";
+  src += "    (void)t;\n";
+  src += body;
+  src += "\n  }\n};\n";
+  for (int m = 0; m < 2; ++m) {
+    for (int tr = 0; tr < 2; ++tr)
+      for (int nt = 0; nt < 2; ++nt)
+        src += "template __global__ void " + rtc_integrate_name(m, tr, nt) + "(const oe::DevProblem, const oe::IntegrateArgs);\n";
+    src += "template __global__ void " + rtc_mh_name(m) + "(const oe::DevProblem, const oe::MHArgs);\n";
+  }
+  return src;
+}
+
+static int compile_program(const std::string& src, const char* arch, std::vector<std::string>& names,
+                           std::vector<std::string>& lowered, std::vector<char>& code, std::string& log) {
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "odelib_user_rhs.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    log = "hiprtcCreateProgram failed";
+    return -1;
+  }
+  for (auto& n : names) hiprtcAddNameExpression(prog, n.c_str());
+  std::string archopt = std::string("--offload-arch=") + arch;
+  const char* opts[] = {archopt.c_str(), "-O3", "-ffp-contract=off", "-std=c++17"};
+  const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+  size_t ls = 0;
+  hiprtcGetProgramLogSize(prog, &ls);
+  log.assign(ls, '\0');
+  if (ls) hiprtcGetProgramLog(prog, &log[0]);
+  if (r != HIPRTC_SUCCESS) {
+    hiprtcDestroyProgram(&prog);
+    return -1;
+  }
+  lowered.clear();
+  for (auto& n : names) {
+    const char* lw = nullptr;
+    if (hiprtcGetLoweredName(prog, n.c_str(), &lw) != HIPRTC_SUCCESS || !lw) {
+      log += "\nno lowered name for " + n;
+      hiprtcDestroyProgram(&prog);
+      return -1;
+    }
+    lowered.emplace_back(lw);
+  }
+  size_t cs = 0;
+  hiprtcGetCodeSize(prog, &cs);
+  code.resize(cs);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  return 0;
+}
+
+static std::vector<std::string> all_names() {
+  std::vector<std::string> names;
+  for (int m = 0; m < 2; ++m)
+    for (int tr = 0; tr < 2; ++tr)
+      for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_integrate_name(m, tr, nt));
+  for (int m = 0; m < 2; ++m) names.push_back(rtc_mh_name(m));
+  return names;
+}
+
+int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule* out, std::string& err) {
+  std::vector<std::string> names = all_names(), lowered;
+  std::vector<char> code;
+  std::string log;
+  if (compile_program(rtc_source(body, S, P), arch, names, lowered, code, log)) {
+    err = "hipRTC compilation of the user RHS failed:\n" + log;
+    return -1;
+  }
+  if (!out) return 0;  // compile check only
+  hipModule_t mod;
+  if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+    err = "hipModuleLoadData failed for the user RHS";
+    return -1;
+  }
+  out->mod = mod;
+  int idx = 0;
+  for (int m = 0; m < 2; ++m)
+    for (int tr = 0; tr < 2; ++tr)
+      for (int nt = 0; nt < 2; ++nt)
+        if (hipModuleGetFunction(&out->integrate[m][tr][nt], mod, lowered[idx++].c_str()) != hipSuccess) {
+          err = "hipModuleGetFunction failed";
+          return -1;
+        }
+  for (int m = 0; m < 2; ++m)
+    if (hipModuleGetFunction(&out->mh[m], mod, lowered[idx++].c_str()) != hipSuccess) {
+      err = "hipModuleGetFunction failed";
+      return -1;
+    }
+  return 0;
+}
+
+}  // namespace oe

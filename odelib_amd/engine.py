@@ -44,6 +44,7 @@ class FitProblem:
     rtol: float = ODEINT_TOL
     atol: float = ODEINT_TOL
     max_steps: int = 500
+    custom_source: str | None = None        # user RHS body for hipRTC (model_id ignored)
 
     def __post_init__(self):
         self.times = np.ascontiguousarray(self.times, dtype=np.float64)
@@ -117,7 +118,10 @@ class Engine:
     # -- problem ---------------------------------------------------------------------------
     def set_problem(self, problem: FitProblem):
         self._sync_stream()
-        self.ctx.problem_set(problem.to_c())
+        c = problem.to_c()
+        if problem.custom_source is not None:  # compiled once per context (cached by source)
+            c.model_id = self.ctx.model_compile(problem.custom_source, problem.n_states, problem.n_params)
+        self.ctx.problem_set(c)
         self.problem = problem
 
     def _sync_stream(self):

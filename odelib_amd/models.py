@@ -10,9 +10,22 @@ of the fit ever comes from the Python callable.
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 import numpy as np
 
 from . import _native as N
+from .transpile import Unsupported, transpile
+
+
+@dataclass
+class DeviceModel:
+    """What the engine runs for a user ODE: a compiled built-in (model_id) or a user
+    RHS body compiled at run time with hipRTC (source)."""
+    name: str
+    n_states: int
+    model_id: int | None = None
+    source: str | None = None
 
 
 # Python statements of the compiled RHS (same operand order as models.cuh), used only
@@ -92,9 +105,26 @@ def _probe_equal(user, ref, n_states, n_params, trials=8, rtol=1e-12):
 
 
 def resolve(ode, n_states: int, n_params: int, device_model: str | None = None):
-    """Return (model_id, n_states) of the compiled RHS equal to ``ode``."""
+    """Return (model_id, n_states) of the compiled built-in RHS equal to ``ode``."""
+    dm = resolve_model(ode, n_states, n_params, device_model, allow_rtc=False)
+    return dm.model_id, dm.n_states
+
+
+def resolve_model(ode, n_states: int, n_params: int, device_model: str | None = None,
+                  device_rhs: str | None = None, allow_rtc: bool = True) -> DeviceModel:
+    """Choose the device RHS for ``ode``:
+
+    1. ``device_rhs`` (C++ body of ``rhs(y, t, ps, dy)``)  -> hipRTC, as given;
+    2. ``device_model`` naming a built-in ('zero_i', 'one_i', 'two_i', 'chain') -> that
+       built-in, after checking the callable computes the same function;
+       ``device_model='rtc'`` forces the transpiled path;
+    3. otherwise the first built-in that agrees with the callable on probe points;
+    4. otherwise the callable transpiled to C (``transpile.py``), checked against the
+       callable on probe points, compiled with hipRTC."""
+    if device_rhs is not None:
+        return DeviceModel("custom-source", n_states, source=device_rhs)
     cands = candidates(n_states, n_params)
-    if device_model is not None:
+    if device_model is not None and device_model != "rtc":
         cands = [c for c in cands if c[0] == device_model]
         if not cands:
             raise ValueError(f"device_model={device_model!r} has no compiled RHS with S={n_states}, "
@@ -102,10 +132,21 @@ def resolve(ode, n_states: int, n_params: int, device_model: str | None = None):
         name, mid, S, P, f = cands[0]
         if ode is not None and not _probe_equal(ode, f, n_states, n_params):
             raise ValueError(f"the ODE callable does not match the compiled {name!r} right-hand side")
-        return mid, S
-    for name, mid, S, P, f in cands:
-        if ode is not None and _probe_equal(ode, f, n_states, n_params):
-            return mid, S
-    raise NotImplementedError(
-        "no compiled device RHS matches this ODE callable; built-ins are "
-        f"{sorted(BUILTIN)} and chain<N> for N in {CHAIN_SIZES} (pass device_model=...)")
+        return DeviceModel(name, S, model_id=mid)
+    if device_model is None:
+        for name, mid, S, P, f in cands:
+            if ode is not None and _probe_equal(ode, f, n_states, n_params):
+                return DeviceModel(name, S, model_id=mid)
+    if not allow_rtc or ode is None:
+        raise NotImplementedError(
+            "no compiled device RHS matches this ODE callable; built-ins are "
+            f"{sorted(BUILTIN)} and chain<N> for N in {CHAIN_SIZES} (pass device_model=... or device_rhs=...)")
+    try:
+        tr = transpile(ode, n_states, n_params)
+    except Unsupported as exc:
+        raise NotImplementedError(
+            f"the ODE callable matches no built-in RHS and cannot be transpiled ({exc}); pass its C body as "
+            "device_rhs='...' (see include/odelib_amd.h oe_model_compile)") from exc
+    if not _probe_equal(ode, tr.evaluate, n_states, n_params):
+        raise NotImplementedError("the transpiled RHS does not reproduce the callable; pass device_rhs='...'")
+    return DeviceModel("rtc:" + getattr(ode, "__name__", "ode"), n_states, source=tr.c_body)

@@ -1,0 +1,97 @@
+"""Python RHS -> C transpiler for the hipRTC path (CPU: translation, validation,
+compile check with hipRTC for gfx950 — no GPU needed)."""
+import math
+
+import numpy as np
+import pytest
+
+from helpers import CONFIGS
+from odelib_amd import _native as N
+from odelib_amd.models import resolve_model
+from odelib_amd.transpile import Unsupported, transpile
+
+K_HALF = 1e6
+
+
+def sat_infection(y, t, ps):
+    """host growth, saturating infection, virus decay, a time-forced term"""
+    mu, phi, beta, delta = ps[0], ps[1], ps[2], ps[3]
+    S, V = y
+    inf = phi * S * V / (1.0 + S / K_HALF)
+    dS = mu * S * (1 - S / 1e7) - inf
+    dV = beta * inf - delta * V + 0.1 * math.sin(2 * np.pi * t) ** 2
+    return [dS, dV]
+
+
+def piecewise(y, t, ps):
+    x = y[0]
+    rate = ps[0] if x < 5.0 else ps[1]
+    out = -rate * x
+    out += np.exp(-x) * 0.0
+    return np.array([out, abs(y[-1]) - np.maximum(x, 1.0) ** 1.5])
+
+
+@pytest.mark.parametrize("name", ["zero_i", "one_i", "two_i"])
+def test_demo_models_translate_exactly(name):
+    f = CONFIGS[name]["ode"]
+    S, P = len(CONFIGS[name]["snames"]), len(CONFIGS[name]["pnames"])
+    tr = transpile(f, S, P)
+    rs = np.random.RandomState(0)
+    for _ in range(20):
+        y = rs.uniform(0, 1e7, S)
+        ps = rs.uniform(0, 2, P) * 10.0 ** rs.uniform(-8, 1, P)
+        assert np.array_equal(tr.evaluate(y, 0.5, ps), np.asarray(f(y, 0.5, ps)))
+    assert "dy[%d]" % (S - 1) in tr.c_body
+
+
+def test_general_subset_translates():
+    tr = transpile(sat_infection, 2, 4)
+    tr2 = transpile(piecewise, 2, 2)
+    rs = np.random.RandomState(1)
+    for _ in range(20):
+        y = rs.uniform(0, 1e7, 2)
+        ps = rs.uniform(0, 1, 4) * [1, 1e-7, 50, 1]
+        t = rs.uniform(0, 3)
+        np.testing.assert_allclose(tr.evaluate(y, t, ps), sat_infection(y, t, ps), rtol=1e-14)
+        y2 = rs.uniform(0, 10, 2)
+        np.testing.assert_allclose(tr2.evaluate(y2, t, ps[:2]), piecewise(y2, t, ps[:2]), rtol=1e-14)
+    assert "1000000.0" in tr.c_body and "sin(" in tr.c_body
+    assert "?" in tr2.c_body and "pow(" in tr2.c_body
+
+
+def test_unsupported_constructs_are_rejected():
+    def loop(y, t, ps):
+        out = []
+        for v in y:
+            out.append(-v)
+        return out
+
+    def dyn_index(y, t, ps):
+        i = 0
+        return [y[i]]
+
+    def wrong_len(y, t, ps):
+        return [y[0]]
+
+    for f, S in ((loop, 2), (dyn_index, 1), (wrong_len, 2)):
+        with pytest.raises(Unsupported):
+            transpile(f, S, 1)
+    with pytest.raises(Unsupported):
+        transpile(lambda y, t, ps: y, 1, 1)
+
+
+def test_resolution_prefers_builtins_then_rtc():
+    dm = resolve_model(CONFIGS["two_i"]["ode"], 4, 5)
+    assert dm.model_id == N.OE_MODEL_TWO_I and dm.source is None
+    dm = resolve_model(CONFIGS["two_i"]["ode"], 4, 5, device_model="rtc")
+    assert dm.model_id is None and "dy[3]" in dm.source
+    dm = resolve_model(sat_infection, 2, 4)
+    assert dm.model_id is None and dm.name == "rtc:sat_infection"
+    dm = resolve_model(None, 3, 2, device_rhs="dy[0] = 0.0; dy[1] = 0.0; dy[2] = 0.0;")
+    assert dm.source.startswith("dy[0]")
+
+
+def test_transpiled_rhs_compiles_with_hiprtc_for_gfx950():
+    N.rtc_check(transpile(sat_infection, 2, 4).c_body, 2, 4, "gfx950")
+    with pytest.raises(ValueError, match="hipRTC compilation"):
+        N.rtc_check("dy[0] = no_such_symbol;", 1, 1, "gfx950")
