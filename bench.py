@@ -180,10 +180,19 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one process per GPU; ODELIB_BENCH_BACKEND=gloo lets several ranks share one GPU to
+    # rehearse the multi-rank path (the driver's N>1 runs use nccl = RCCL over xGMI)
+    backend = os.environ.get("ODELIB_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank % max(ndev, 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     eng = m.engine()
     fp = eng.problem
@@ -216,7 +225,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = [a.elapsed_time(b) for a, b in ev]
@@ -244,16 +253,16 @@ def main():
         t_ag = 0.0
         gathered_bytes = r["samples"].numel() * 8 * n_gpus
         if world > 1:
-            blk = r["samples"].contiguous()
-            gath = torch.empty((world,) + tuple(blk.shape), dtype=blk.dtype, device=dev)
+            from odelib_amd.distributed import allgather_walkers
+            blk = r["samples"].contiguous() if backend == "nccl" else r["samples"].cpu()
             dist.barrier()
             torch.cuda.synchronize(dev)
             ta = time.perf_counter()
-            dist.all_gather_into_tensor(gath, blk)
+            pooled = allgather_walkers(blk, Wl * n_gpus)  # Framework.py:1037 pd.concat analogue
             torch.cuda.synchronize(dev)
             t_ag = time.perf_counter() - ta
-        if world > 1:
-            tt = torch.tensor([t_mh, t_ag], dtype=torch.float64, device=dev)
+            assert pooled.shape[-1] == Wl * n_gpus
+            tt = torch.tensor([t_mh, t_ag], dtype=torch.float64, device=red_dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             t_mh, t_ag = float(tt[0]), float(tt[1])
         mh_wts = n_gpus * Wl * (T - 1) * nits  # a-priori integrate + nits-1 proposals
@@ -261,7 +270,7 @@ def main():
         mcmc = {"iterations": nits, "walker_timesteps_per_s": mh_wts / t_mh, "kernel_ms": mh_kernel_ms,
                 "fp64_tflops_est": Wl * (T - 1) * nits * flops_per_wts * (S / 4.0) / (mh_kernel_ms / 1e3) / 1e12,
                 "fp64_peak_tflops": FP64_VALU_TFS, "allgather_s": t_ag, "allgather_bytes": gathered_bytes,
-                "rng": "philox"}
+                "allgather_backend": backend if world > 1 else None, "rng": "philox"}
 
     if rank == 0:
         line = {
