@@ -5,8 +5,8 @@ src = open(sys.argv[1]).read()
 keep = []
 for line in src.splitlines():
     s = line.strip()
-    if s.startswith("#include") or s == "#pragma once":
-        continue
+    if s.startswith("#include") or s == "#pragma once" or s.startswith("//"):
+        continue  # includes are provided by hipRTC; comments are not needed at run time
     keep.append(line)
 body = "\n".join(keep)
 assert ")OE_RTC\"" not in body

@@ -80,6 +80,45 @@ __global__ void __launch_bounds__(256) buf_kernel(double* out, long W, int T, in
   }
 }
 
+// L4: walker-tiled [W/64][T][S][64] through a per-wave buffer descriptor (contiguous
+// 2 KB per wave per step), cache-policy bits AUX
+template <int AUX, int S>
+__global__ void __launch_bounds__(256) tiled_kernel(double* out, long W, int T, int work, double a) {
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  const long gw = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gw >= W) return;
+  double y[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) y[s] = 1.0 + 1e-3 * s + 1e-9 * (double)gw;
+  const long tile = gw >> 6;
+  auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(out + tile * (long)T * S * 64), 0, (unsigned)(T * S * 64 * 8), 0x00020000);
+  const unsigned lane_off = (unsigned)(gw & 63) * 8u;
+  for (int t = 0; t < T; ++t) {
+    for (int k = 0; k < work; ++k) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) y[s] = fma(y[s], a, 1e-7);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, y[s]), rsrc, lane_off, (unsigned)((t * S + s) * 512), AUX);
+  }
+}
+
+template <int AUX>
+float runtiled(double* out, long W, int T, int work, int reps) {
+  dim3 g((unsigned)((W + 255) / 256)), b(256);
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((tiled_kernel<AUX, 4>), g, b, 0, 0, out, W, T, work, 0.999999);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((tiled_kernel<AUX, 4>), g, b, 0, 0, out, W, T, work, 0.999999);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+
 template <int AUX>
 float runbuf(double* out, long W, int T, int work, int reps) {
   dim3 g((unsigned)((W + 255) / 256)), b(256);
@@ -127,6 +166,11 @@ int main(int argc, char** argv) {
     printf("work=%2d fma/step/state | L0 %.3f ms %.2f TB/s | L0nt %.3f %.2f | L1 %.3f %.2f | L1nt %.3f %.2f | "
            "L2 %.3f %.2f | L2nt %.3f %.2f\n",
            work, t00, bw(t00), t01, bw(t01), t10, bw(t10), t11, bw(t11), t20, bw(t20), t21, bw(t21));
+  }
+  for (int work : {0, 8, 14}) {
+    auto bw = [&](float ms) { return bytes / (ms * 1e-3) / 1e12; };
+    float b0 = runbuf<2>(out, W, T, work, reps), t0 = runtiled<2>(out, W, T, work, reps), t1 = runtiled<0>(out, W, T, work, reps);
+    printf("work=%2d | rowbuf nt %.3f ms %.2f | tiled nt %.3f %.2f | tiled cached %.3f %.2f TB/s\n", work, b0, bw(b0), t0, bw(t0), t1, bw(t1));
   }
   for (int work : {0, 14}) {
     auto bw = [&](float ms) { return bytes / (ms * 1e-3) / 1e12; };
