@@ -283,6 +283,29 @@ constexpr double d1 = -12715105075.0 / 11282082432.0, d3 = 87487479700.0 / 32700
                  d4 = -10690763975.0 / 1880347072.0, d5 = 701980252875.0 / 199316789632.0,
                  d6 = -1453857185.0 / 822651844.0, d7 = 69997945.0 / 29380423.0;
 constexpr double safe = 0.9, facmin = 0.2, facmax = 10.0;
+
+// x^(-1/5) for finite x > 0 (the step controller's err^(-1/5) and HINIT's
+// (0.01/dm)^(1/5)).  Only exact scalings (frexp/ldexp) and IEEE mul/fma, so the host
+// restatement (oracle/rk_ref.c inv_fifth_root) reproduces it bit for bit — libm's and
+// ocml's pow/exp/log do not agree to the last ulp — and it is ~25 VALU ops instead
+// of an exp(log()) pair.  x = m·2^e, e = 5q + r: x^(-1/5) = m^(-1/5)·2^(-r/5)·2^(-q);
+// m^(-1/5) on [0.5, 1) from a quadratic start (1.5e-3) and two Newton steps (1.5e-10).
+__device__ __forceinline__ double inv_fifth_root(double x) {
+  int e;
+  const double m = frexp(x, &e);
+  int q = e / 5, r = e % 5;
+  if (r < 0) { r += 5; q -= 1; }
+  double y = fma(fma(0.2395, m, -0.6505), m, 1.4123);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double y2 = y * y;
+    const double y5 = (y2 * y2) * y;
+    y = (y * fma(-m, y5, 6.0)) * 0.2;
+  }
+  const double c = r == 0 ? 1.0 : r == 1 ? 0.8705505632961241 : r == 2 ? 0.757858283255199
+                 : r == 3 ? 0.6597539553864471 : 0.5743491774985174;
+  return ldexp(c * y, -q);
+}
 }  // namespace dp
 
 template <class M, int PMAX, bool TRAJ, bool NT>
@@ -325,7 +348,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
     }
     d2 = d2 / h0;
     const double dm = fmax(d1v, d2);
-    const double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / dm, 0.2);
+    const double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : inv_fifth_root(dm / 0.01);
     double hl = fmin(100.0 * h0, h1);
     if (dead || !__builtin_isfinite(hl) || !(hl > 0.0)) hl = tend - t0;
     h = wave_min(hl);
@@ -393,6 +416,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
       // per grid point (four more S-vectors would spill)
       constexpr bool kHoist = S <= 8;
       bool have_dense = false;
+      const double rh = 1.0 / h;  // one division per step, not per grid point
       double ydf[kHoist ? S : 1], bsp[kHoist ? S : 1], r4[kHoist ? S : 1], r5[kHoist ? S : 1];
       const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
       while (i < pb.T && times[i] <= tn) {
@@ -403,7 +427,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
             for (int s = 0; s < S; ++s) yo[s] = yn[s];
           } else {
-            const double th = (ti - t) / h;
+            const double th = (ti - t) * rh;
             const double th1 = 1.0 - th;
             if constexpr (kHoist) {
               if (!have_dense) {
@@ -442,13 +466,13 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
       for (int s = 0; s < S; ++s) { y[s] = yn[s]; k1[s] = k7[s]; }
       t = tn;
-      double fac = (err > 0.0) ? safe * exp(-0.2 * log(err)) : facmax;
+      double fac = (err > 0.0) ? safe * inv_fifth_root(err) : facmax;
       fac = fmin(facmax, fmax(facmin, fac));
       if (last_rej) fac = fmin(fac, 1.0);
       h = h * fac;
       last_rej = false;
     } else {
-      h = h * fmax(facmin, safe * exp(-0.2 * log(err)));
+      h = h * fmax(facmin, safe * inv_fifth_root(err));
       last_rej = true;
     }
     // ---- budget: evict the walkers that pin the wave's step ----

@@ -190,6 +190,25 @@ typedef struct {
   int kobs;
 } Lane;
 
+/* x^(-1/5), same operations as ode_kernels.cuh inv_fifth_root (bit-identical) */
+static double inv_fifth_root(double x) {
+  int e;
+  const double m = frexp(x, &e);
+  int q = e / 5, r = e % 5;
+  if (r < 0) { r += 5; q -= 1; }
+  double y = fma(fma(0.2395, m, -0.6505), m, 1.4123);
+  for (int it = 0; it < 2; ++it) {
+    const double y2 = y * y;
+    const double y5 = (y2 * y2) * y;
+    y = (y * fma(-m, y5, 6.0)) * 0.2;
+  }
+  const double c = r == 0 ? 1.0 : r == 1 ? 0.8705505632961241 : r == 2 ? 0.757858283255199
+                 : r == 3 ? 0.6597539553864471 : 0.5743491774985174;
+  return ldexp(c * y, -q);
+}
+
+double ref_inv_fifth_root(double x) { return inv_fifth_root(x); }
+
 static double grp_max(Lane* L, int n, int use_dead_zero) {
   double m = 0.0;
   (void)use_dead_zero;
@@ -230,7 +249,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     }
     d2 = d2 / h0;
     double dm = fmax(d1v, d2);
-    double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / dm, 0.2);
+    double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : inv_fifth_root(dm / 0.01);
     double hl = fmin(100.0 * h0, h1);
     if (q->dead || !isfinite(hl) || !(hl > 0.0)) hl = tend - t0;
     h = fmin(h, hl);
@@ -286,6 +305,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     ++nst;
     if (err <= 1.0) {
       double tn = last ? tend : t + h;
+      const double rh = 1.0 / h;
       const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
       while (i < pb->T && pb->times[i] <= tn) {
         for (int l = 0; l < nl; ++l) {
@@ -296,7 +316,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
           if (ti == tn) {
             for (int s = 0; s < S; ++s) yo[s] = q->yn[s];
           } else {
-            double th = (ti - t) / h, th1 = 1.0 - th;
+            double th = (ti - t) * rh, th1 = 1.0 - th;
             for (int s = 0; s < S; ++s) {
               double ydf = q->yn[s] - q->y[s];
               double bsp = fma(h, q->k1[s], -ydf);
@@ -317,13 +337,13 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
         memcpy(L[l].k1, L[l].k7, sizeof(double) * S);
       }
       t = tn;
-      double fac = (err > 0.0) ? 0.9 * exp(-0.2 * log(err)) : 10.0;
+      double fac = (err > 0.0) ? 0.9 * inv_fifth_root(err) : 10.0;
       fac = fmin(10.0, fmax(0.2, fac));
       if (last_rej) fac = fmin(fac, 1.0);
       h = h * fac;
       last_rej = 0;
     } else {
-      h = h * fmax(0.2, 0.9 * exp(-0.2 * log(err)));
+      h = h * fmax(0.2, 0.9 * inv_fifth_root(err));
       last_rej = 1;
     }
     if (nst >= pb->max_steps || h < hmin) {

@@ -32,6 +32,8 @@ def lib():
         L.ref_mh.restype = C.c_int
         L.ref_mh.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, d, d, i32, d, i32,
                              i64, i64, i32, i32, i32, u64, d, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ref_inv_fifth_root.restype = d
+        L.ref_inv_fifth_root.argtypes = [d]
         L.ref_philox4x32_10.restype = None
         L.ref_philox4x32_10.argtypes = [vp, vp, vp]
         L.ref_philox_draws.restype = None
@@ -110,6 +112,11 @@ def mh_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, rng="philox"
     if rc:
         raise RuntimeError("ref_mh failed")
     return {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status}
+
+
+def inv_fifth_root(x: float) -> float:
+    """x^(-1/5) as the DOPRI5 step controller computes it (oracle/rk_ref.c)."""
+    return lib().ref_inv_fifth_root(float(x))
 
 
 def philox4x32_10(ctr, key):

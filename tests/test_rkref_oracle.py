@@ -17,6 +17,17 @@ def test_philox_known_answers():
                                      [0xa4093822, 0x299f31d0])) == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
 
 
+def test_inv_fifth_root_accuracy():
+    """The step controller's x^(-1/5) (exact scalings + mul/fma only, so host and device
+    agree bitwise) is within 1e-9 of the true value from denormals to 1e30."""
+    xs = np.concatenate([[5e-324, 1e-310, 2.2250738585072014e-308, 1e-30, 1.0, 1e30],
+                         np.logspace(-300, 300, 4001), np.random.RandomState(1).uniform(0.5, 40.0, 2000)])
+    for x in xs:
+        got = rk_ref.inv_fifth_root(x)
+        want = float(np.float64(x) ** -0.2) if x > 1e-300 else float(np.exp(-0.2 * np.log(np.longdouble(x))))
+        assert abs(got / want - 1.0) < 1e-9, (x, got, want)
+
+
 def _inputs(name, W=8):
     m = product_model(name)
     fp = m.fit_problem()

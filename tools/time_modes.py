@@ -1,0 +1,50 @@
+"""Kernel time of one batched integrate with and without the trajectory store, per
+model / method / walker count: separates the compute floor from the store floor.
+
+    python tools/time_modes.py --cases two_i:rk4:65536 two_i:dopri5:65536 chain20:dopri5:262144
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", nargs="+", default=["two_i:rk4:65536", "two_i:dopri5:65536"])
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import bench
+    dev = torch.device("cuda:0")
+    for case in args.cases:
+        model, method, W = case.split(":")
+        W = int(W)
+        m, y0h = bench.build_problem(model, method, 1000)
+        eng = m.engine()
+        S, P = len(y0h), 5
+        theta = torch.as_tensor(bench.synthetic_walkers(W, P), device=dev).contiguous()
+        y0 = torch.as_tensor(np.repeat(y0h[:, None], W, axis=1), device=dev).contiguous()
+        traj = eng.empty_traj(W)
+        row = {"case": case}
+        for mode in ("traj", "notraj"):
+            ms = []
+            for r in range(args.reps + 2):
+                if mode == "traj":
+                    eng.integrate(y0, theta, trajectory=True, traj_out=traj, sync=True)
+                else:
+                    eng.integrate(y0, theta, trajectory=False, sync=True)
+                if r >= 2:
+                    ms.append(eng.last_kernel_ms())
+            row[mode + "_ms"] = round(float(np.median(ms)), 4)
+        row["store_floor_ms"] = round(W * 999 * 8 * S / 6.3e12 * 1e3, 4)
+        row["hbm_frac_traj"] = round(W * 999 * 8 * S / (row["traj_ms"] * 1e-3) / 8e12, 4)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
