@@ -157,6 +157,29 @@ def cpu_baseline(model, fp, y0, budget_s, P):
                       f"CPU: {cpu_model}"}
 
 
+def cpu_rk4_c(fp, y0, W, cores):
+    """The same fixed-step RK4 + fused likelihood in C (oracle/rk_ref.c, OpenMP over
+    64-walker groups, interval-major so rows are written as runs of walkers) on the
+    full bench workload: the apples-to-apples CPU number for the GPU kernel (SURVEY
+    §8d).  Runs in this process after the fork pool and before GPU initialisation."""
+    import numpy as np
+    os.environ["OMP_NUM_THREADS"] = str(cores)
+    from oracle import rk_ref
+    theta = synthetic_walkers(W, 5)
+    Y0 = np.ascontiguousarray(np.repeat(y0[:, None], W, axis=1))
+    rk_ref.integrate(fp, Y0[:, :64 * cores].copy(), theta[:, :64 * cores].copy())  # threads up, pages in
+    best = None
+    for _ in range(2):
+        t0 = time.perf_counter()
+        rk_ref.integrate(fp, Y0, theta, trajectory=True)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    T = len(fp.times)
+    return {"value": W * (T - 1) / best, "unit": "walker-timesteps/s", "cores": cores, "kind": "port",
+            "sample": f"{W} walkers x {T - 1} intervals, RK4 + trajectory store + chi in C "
+                      f"(oracle/rk_ref.c, gcc -O2, OpenMP {cores} threads), best of 2: {best:.2f} s"}
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
@@ -172,6 +195,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.model, fp_host, y0h, args.cpu_seconds, P)
+        if args.method == "rk4":
+            cpu["rk4_c_openmp"] = cpu_rk4_c(fp_host, y0h, args.walkers, cpu["cores"])
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     if world == 1 and not args.no_pmc:
         traffic, traffic_note = pmc_traffic(args)

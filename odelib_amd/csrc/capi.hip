@@ -88,6 +88,8 @@ struct oe_ctx {
   // scratch
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  void* draws = nullptr;  // philox proposal draws of one MH chunk
+  size_t draws_bytes = 0;
 };
 
 namespace {
@@ -120,12 +122,31 @@ int ensure_scratch(oe_ctx* c, size_t bytes) {
   return OE_OK;
 }
 
+int ensure_draws(oe_ctx* c, size_t bytes) {
+  if (c->draws_bytes >= bytes) return OE_OK;
+  if (c->draws) {
+    OE_HIP(c, hipStreamSynchronize(c->stream));
+    OE_HIP(c, hipFree(c->draws));
+    c->draws = nullptr;
+    c->draws_bytes = 0;
+  }
+  OE_HIP(c, hipMalloc(&c->draws, bytes));
+  c->draws_bytes = bytes;
+  return OE_OK;
+}
+
 int set_device(oe_ctx* c) {
   OE_HIP(c, hipSetDevice(c->device));
   return OE_OK;
 }
 
 }  // namespace
+
+// MH proposal draws (philox mode), one lane per walker; see oe::philox_draws
+__global__ void __launch_bounds__(256) k_philox_draws(const oe::DrawArgs d) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < d.W) oe::philox_draws(d, w);
+}
 
 extern "C" {
 
@@ -182,6 +203,7 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->d_obs) (void)hipFree(c->d_obs);
     if (c->d_rk4) (void)hipFree(c->d_rk4);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->draws) (void)hipFree(c->draws);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (auto& m : c->custom)
@@ -444,10 +466,6 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   m.W = W;
   m.walker_offset = a->walker_offset;
   m.burnin = a->burnin;
-  m.rng_mode = a->rng_mode;
-  m.seed_lo = (uint32_t)a->seed;
-  m.seed_hi = (uint32_t)(a->seed >> 32);
-  m.step_sd = a->step_sd;
   m.walk_mask = 0;
   for (int p = 0; p < P; ++p)
     if (a->walk_mask[p]) m.walk_mask |= (1ull << p);
@@ -458,8 +476,6 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
     if (ip < -1 || ip >= P) return fail(c, OE_ERR_ARG, "oe_mh_run: init_param out of range");
     m.init_param[s] = ip;
   }
-  m.replay_dz = a->replay_dz;
-  m.replay_u = a->replay_u;
   m.theta = a->theta;
   m.y0 = a->y0;
   m.samples = a->samples;
@@ -474,7 +490,30 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   }
 
   const dim3 grid((unsigned)((W + kBlock - 1) / kBlock)), block(kBlock);
-  const int chunk = a->chunk > 0 ? a->chunk : 25;
+  int chunk = a->chunk > 0 ? a->chunk : 25;
+  const bool philox = a->rng_mode == OE_RNG_PHILOX;
+  DrawArgs d{};
+  if (philox && a->nits > 1) {
+    // one chunk of draws resident at a time, at most ~1 GiB (at least one iteration)
+    const size_t per_it = sizeof(double) * (size_t)(P + 1) * (size_t)W;
+    chunk = (int)std::max<int64_t>(1, std::min<int64_t>(chunk, (int64_t)((1ull << 30) / per_it)));
+    rc = ensure_draws(c, per_it * (size_t)chunk);
+    if (rc) return rc;
+    d.W = W;
+    d.walker_offset = a->walker_offset;
+    d.P = P;
+    d.seed_lo = (uint32_t)a->seed;
+    d.seed_hi = (uint32_t)(a->seed >> 32);
+    d.step_sd = a->step_sd;
+    d.dz = static_cast<double*>(c->draws);
+    d.u = d.dz + (size_t)chunk * P * W;
+    m.dz = d.dz;
+    m.u = d.u;
+  } else {
+    m.dz = a->replay_dz;
+    m.u = a->replay_u;
+    m.draw_it0 = 1;
+  }
   OE_HIP(c, hipEventRecord(c->ev0, c->stream));
   m.init = 1;
   m.it0 = 0;
@@ -484,6 +523,13 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   for (int it0 = 1; it0 < a->nits; it0 += chunk) {
     m.it0 = it0;
     m.it1 = std::min(a->nits, it0 + chunk);
+    if (philox) {
+      d.it0 = m.it0;
+      d.it1 = m.it1;
+      m.draw_it0 = it0;
+      hipLaunchKernelGGL(k_philox_draws, grid, block, 0, c->stream, d);
+      OE_HIP(c, hipGetLastError());
+    }
     OE_HIP(c, launch_mh_entry(e, c->method, c->dp, m, grid, block, c->stream));
   }
   OE_HIP(c, hipEventRecord(c->ev1, c->stream));

@@ -184,6 +184,16 @@ __device__ __forceinline__ void observe(const DevProblem& pb, int i, const doubl
   }
 }
 
+// observe() with the next observed grid index carried in a (uniform) register, so a
+// grid point without an observation costs a compare instead of a scalar load + wait.
+template <int S>
+__device__ __forceinline__ void observe_next(const DevProblem& pb, int i, const double (&y)[S], int& k,
+                                             int& nxt, Acc& a) {
+  if (i != nxt) return;
+  observe<S>(pb, i, y, k, a);
+  nxt = (k < pb.n_obs) ? kconst(pb.obs)[k].tidx : 0x7fffffff;
+}
+
 // Emit grid point i: row store + minimum + observations.
 template <int S, bool TRAJ, bool NT>
 __device__ __forceinline__ void emit(const DevProblem& pb, int i, const double (&y)[S],
@@ -357,7 +367,13 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 
   const double span = tend - t0;
   const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
+  // S <= 8: times[i] loaded one grid point ahead, next observed index carried, evicted
+  // lanes poisoned with NaN (no per-point select).  S > 8 sits at the register limit,
+  // so it keeps the leaner form (same outputs and status bits).
+  constexpr bool kLean = S > 8;
   int i = 1;
+  double t_i = times[1];
+  int nxt = (k < pb.n_obs) ? kconst(pb.obs)[k].tidx : 0x7fffffff;  // next observed index
   int nst = 0;  // steps since the last grid point
   bool last_rej = false;
   while (i < pb.T) {
@@ -419,10 +435,11 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
       const double rh = 1.0 / h;  // one division per step, not per grid point
       double ydf[kHoist ? S : 1], bsp[kHoist ? S : 1], r4[kHoist ? S : 1], r5[kHoist ? S : 1];
       const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
-      while (i < pb.T && times[i] <= tn) {
-        if (grid_needs_emit<S, TRAJ>(pb, i, k)) {
+      while (i < pb.T && (kLean ? times[i] : t_i) <= tn) {
+        const double ti = kLean ? times[i] : t_i;
+        if constexpr (!kLean) t_i = times[i + 1 < pb.T ? i + 1 : i];  // issued now, used next iteration
+        if (kLean ? grid_needs_emit<S, TRAJ>(pb, i, k) : (TRAJ || i == nxt)) {
           double yo[S];
-          const double ti = times[i];
           if (ti == tn) {
 #pragma unroll
             for (int s = 0; s < S; ++s) yo[s] = yn[s];
@@ -454,11 +471,17 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
               }
             }
           }
-          if (dead) {
+          if constexpr (kLean) {
+            if (dead) {
 #pragma unroll
-            for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
+              for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
+            }
+            emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
+          } else {
+            // (an evicted lane's state is NaN, so its dense output is NaN already)
+            store_row<S, TRAJ, NT>(i, yo, traj, W, off, active, a);
+            observe_next<S>(pb, i, yo, k, nxt, a);
           }
-          emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
         }
         ++i;
         nst = 0;
@@ -477,7 +500,15 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
     }
     // ---- budget: evict the walkers that pin the wave's step ----
     if (nst >= pb.max_steps || h < hmin) {
-      if (!dead && el >= 0.5 * err) { dead = true; a.status |= ST_MAXSTEP; }
+      if (!dead && el >= 0.5 * err) {
+        dead = true;
+        a.status |= ST_MAXSTEP;
+        // poison the lane: every later dense output (and the final state) is NaN
+        if constexpr (!kLean) {
+#pragma unroll
+          for (int s = 0; s < S; ++s) { y[s] = __builtin_nan(""); k1[s] = __builtin_nan(""); }
+        }
+      }
       nst = pb.max_steps / 2;
       if (__ballot(!dead) == 0ull) {
         // every lane is out: emit NaN rows for the rest of the grid and stop
@@ -493,6 +524,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
   }
   if (dead && active) a.status |= ST_MAXSTEP;
   check_finite(y, a);
+  if (kLean && dead) a.nf = __builtin_nan("");  // as if poisoned: final state non-finite
 }
 
 template <class M, int PMAX, int METHOD, bool TRAJ, bool NT>
@@ -698,6 +730,43 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
 
+// Proposal draws of iterations [it0, it1) for every walker, in the layout of the
+// replay streams: dz[it - it0][p][w] = step_sd * N(0,1), u[it - it0][w] = U[0,1).
+// Counter (global walker id, iteration, pair index) under key = seed, so the draws do
+// not depend on how walkers are sharded or iterations chunked.  Its own kernel, so the
+// MH kernel carries no Box–Muller transcendentals (register pressure).
+struct DrawArgs {
+  int64_t W;
+  int64_t walker_offset;
+  int32_t it0, it1;
+  int32_t P;
+  uint32_t seed_lo, seed_hi;
+  double step_sd;
+  double* dz;  // [it1 - it0][P][W]
+  double* u;   // [it1 - it0][W]
+};
+
+__device__ __forceinline__ void philox_draws(const DrawArgs d, int64_t w) {
+  const uint64_t gid = (uint64_t)(d.walker_offset + w);
+  const int64_t W = d.W;
+  for (int it = d.it0; it < d.it1; ++it) {
+    double* dz = d.dz + (int64_t)(it - d.it0) * d.P * W + w;
+    for (int j = 0; j < d.P; j += 2) {
+      const U4 r = philox4x32_10(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, (uint32_t)(j >> 1)},
+                                 d.seed_lo, d.seed_hi);
+      const double u1 = 1.0 - u53(r.x, r.y);
+      const double u2 = u53(r.z, r.w);
+      const double rad = sqrt(-2.0 * log(u1));
+      const double ang = 6.283185307179586 * u2;
+      dz[(int64_t)j * W] = d.step_sd * (rad * cos(ang));
+      if (j + 1 < d.P) dz[(int64_t)(j + 1) * W] = d.step_sd * (rad * sin(ang));
+    }
+    const U4 r = philox4x32_10(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, 0x80000000u},
+                               d.seed_lo, d.seed_hi);
+    d.u[(int64_t)(it - d.it0) * W + w] = u53(r.x, r.y);
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // Kernel 2: Metropolis–Hastings, iterations [it0, it1) for every walker
 // (Samplers.py:104-153).  One lane = one chain; the chain state lives in HBM
@@ -708,15 +777,13 @@ struct MHArgs {
   int64_t walker_offset;
   int32_t it0, it1;        // iteration range of this launch (1-based, ref `it`)
   int32_t burnin;
-  int32_t rng_mode;        // 0 replay, 1 philox
+  int32_t draw_it0;        // iteration whose draws sit at offset 0 of dz/u
   int32_t init;            // 1: compute the a-priori chi/R²/AIC only (Samplers.py:88-91)
   int32_t any_walk;
   uint64_t walk_mask;      // bit p: parameter p walks
-  uint32_t seed_lo, seed_hi;
-  double step_sd;
   int32_t init_param[64];  // per state: -1 or parameter index
-  const double* replay_dz; // [nits-1][P][W]
-  const double* replay_u;  // [nits-1][W]
+  const double* dz;        // [..][P][W] step_sd·N(0,1) (replay streams or philox_draws)
+  const double* u;         // [..][W]
   double* theta;           // [P][W]
   double* y0;              // [S][W]
   double* samples;         // [kept][P+5][W]
@@ -759,39 +826,16 @@ __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma
   double chi = ma.cur[w], rsq = ma.cur[W + w], aic = ma.cur[2 * W + w];
   double nacc = ma.cur[3 * W + w];
   int32_t status = ma.status ? ma.status[w] : 0;
-  const uint64_t gid = (uint64_t)(ma.walker_offset + w);
   const int PS = P + 5;
 
   for (int it = ma.it0; it < ma.it1; ++it) {
     // ---- proposal: θ' = exp(log θ + N(0, sd)) for walking parameters (Framework.py:107-122)
     double tn[PMAX];
-    double u;
-    if (ma.rng_mode == 0) {
-      const double* dz = ma.replay_dz + (int64_t)(it - 1) * P * W + w;
+    const double* dz = ma.dz + (int64_t)(it - ma.draw_it0) * P * W + w;
 #pragma unroll
-      for (int j = 0; j < PMAX; ++j)
-        tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? exp(log(th[j]) + dz[(int64_t)j * W]) : th[j];
-      u = ma.replay_u[(int64_t)(it - 1) * W + w];
-    } else {
-      double z[PMAX + 1];
-#pragma unroll
-      for (int j = 0; j < PMAX; j += 2) {
-        const U4 r = philox4x32_10(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, (uint32_t)(j >> 1)},
-                                   ma.seed_lo, ma.seed_hi);
-        const double u1 = 1.0 - u53(r.x, r.y);
-        const double u2 = u53(r.z, r.w);
-        const double rad = sqrt(-2.0 * log(u1));
-        const double ang = 6.283185307179586 * u2;
-        z[j] = rad * cos(ang);
-        z[j + 1] = rad * sin(ang);
-      }
-      const U4 r = philox4x32_10(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, 0x80000000u},
-                                 ma.seed_lo, ma.seed_hi);
-      u = u53(r.x, r.y);
-#pragma unroll
-      for (int j = 0; j < PMAX; ++j)
-        tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? exp(log(th[j]) + ma.step_sd * z[j]) : th[j];
-    }
+    for (int j = 0; j < PMAX; ++j)
+      tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? exp(log(th[j]) + dz[(int64_t)j * W]) : th[j];
+    const double u = ma.u[(int64_t)(it - ma.draw_it0) * W + w];
     // '<state>0' parameters drive initial states (Samplers.py:110-114)
     double y[S], yp0[S];
 #pragma unroll

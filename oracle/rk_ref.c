@@ -139,33 +139,24 @@ static int needs_emit(const Prob* pb, int traj, int i, int k) {
   return traj || (k < pb->n_obs && pb->obs_tidx[k] == i);
 }
 
-/* ---- fixed-step RK4 ---- */
-static void rk4_walker(const Prob* pb, double* y, const double* p, double* traj, int64_t W, int64_t w, Acc* a) {
+/* ---- fixed-step RK4, one walker advanced over one output interval ---- */
+static void rk4_interval(const Prob* pb, double* y, const double* p, double t, double t1) {
   const int S = pb->S;
   double k[MAXS], acc[MAXS], yt[MAXS];
-  int kk = 0;
-  emit(pb, 0, y, traj, W, w, &kk, a);
-  double t = pb->times[0];
   const int n = pb->substeps;
-  for (int i = 1; i < pb->T; ++i) {
-    double t1 = pb->times[i];
-    double h = (t1 - t) / (double)n;
-    for (int j = 0; j < n; ++j) {
-      double ts = t + (double)j * h;
-      double hh = 0.5 * h, h6 = h / 6.0;
-      rhs(pb, y, ts, p, k);
-      for (int s = 0; s < S; ++s) { acc[s] = k[s]; yt[s] = fma(hh, k[s], y[s]); }
-      rhs(pb, yt, ts + hh, p, k);
-      for (int s = 0; s < S; ++s) { acc[s] = fma(2.0, k[s], acc[s]); yt[s] = fma(hh, k[s], y[s]); }
-      rhs(pb, yt, ts + hh, p, k);
-      for (int s = 0; s < S; ++s) { acc[s] = fma(2.0, k[s], acc[s]); yt[s] = fma(h, k[s], y[s]); }
-      rhs(pb, yt, ts + h, p, k);
-      for (int s = 0; s < S; ++s) { acc[s] = acc[s] + k[s]; y[s] = fma(h6, acc[s], y[s]); }
-    }
-    t = t1;
-    if (needs_emit(pb, traj != NULL, i, kk)) emit(pb, i, y, traj, W, w, &kk, a);
+  double h = (t1 - t) / (double)n;
+  for (int j = 0; j < n; ++j) {
+    double ts = t + (double)j * h;
+    double hh = 0.5 * h, h6 = h / 6.0;
+    rhs(pb, y, ts, p, k);
+    for (int s = 0; s < S; ++s) { acc[s] = k[s]; yt[s] = fma(hh, k[s], y[s]); }
+    rhs(pb, yt, ts + hh, p, k);
+    for (int s = 0; s < S; ++s) { acc[s] = fma(2.0, k[s], acc[s]); yt[s] = fma(hh, k[s], y[s]); }
+    rhs(pb, yt, ts + hh, p, k);
+    for (int s = 0; s < S; ++s) { acc[s] = fma(2.0, k[s], acc[s]); yt[s] = fma(h, k[s], y[s]); }
+    rhs(pb, yt, ts + h, p, k);
+    for (int s = 0; s < S; ++s) { acc[s] = acc[s] + k[s]; y[s] = fma(h6, acc[s], y[s]); }
   }
-  check_finite(S, y, a);
 }
 
 /* ---- DOPRI5 over one 64-lane group in lockstep ---- */
@@ -348,7 +339,11 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     }
     if (nst >= pb->max_steps || h < hmin) {
       for (int l = 0; l < nl; ++l)
-        if (!L[l].dead && L[l].el >= 0.5 * err) { L[l].dead = 1; L[l].a.status |= ST_MAXSTEP; }
+        if (!L[l].dead && L[l].el >= 0.5 * err) {
+          L[l].dead = 1;
+          L[l].a.status |= ST_MAXSTEP;
+          for (int s = 0; s < S; ++s) L[l].y[s] = L[l].k1[s] = NAN; /* evicted: NaN from here on */
+        }
       nst = pb->max_steps / 2;
       int alive = 0;
       for (int l = 0; l < nl; ++l) alive |= !L[l].dead;
@@ -394,8 +389,20 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
     for (int j = 0; j < MAXP; ++j) p[l * MAXP + j] = (j < P) ? theta[(int64_t)j * W + w] : 0.0;
   }
   if (pb->method == 0) {
+    /* interval-major over the group, so each trajectory row is written as runs of
+       consecutive walkers (per-walker arithmetic unchanged) */
     for (int l = 0; l < LANES; ++l)
-      if (L[l].active) rk4_walker(pb, L[l].y, p + l * MAXP, traj, W, L[l].w, &L[l].a);
+      if (L[l].active) { L[l].kobs = 0; emit(pb, 0, L[l].y, traj, W, L[l].w, &L[l].kobs, &L[l].a); }
+    for (int i = 1; i < pb->T; ++i) {
+      const double t = pb->times[i - 1], t1 = pb->times[i];
+      for (int l = 0; l < LANES; ++l) {
+        if (!L[l].active) continue;
+        rk4_interval(pb, L[l].y, p + l * MAXP, t, t1);
+        if (needs_emit(pb, traj != NULL, i, L[l].kobs)) emit(pb, i, L[l].y, traj, W, L[l].w, &L[l].kobs, &L[l].a);
+      }
+    }
+    for (int l = 0; l < LANES; ++l)
+      if (L[l].active) check_finite(pb->S, L[l].y, &L[l].a);
   } else {
     dopri5_group(pb, L, LANES, p, traj, W);
   }
@@ -408,8 +415,11 @@ int ref_integrate(int model, int S, int P, int T, const double* times, int n_obs
                   const double* theta, double* traj, double* chi, double* ssres, int32_t* status) {
   if (S > MAXS || P > MAXP || W <= 0) return -1;
   Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
-  Acc acc[LANES];
-  for (int64_t g = 0; g * LANES < W; ++g) {
+  const int64_t ngroups = (W + LANES - 1) / LANES;
+  /* groups are independent: OpenMP over groups gives the same bits as the serial loop */
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int64_t g = 0; g < ngroups; ++g) {
+    Acc acc[LANES];
     integrate_group(&pb, W, g, y0, theta, traj, acc);
     for (int l = 0; l < LANES; ++l) {
       int64_t w = g * LANES + l;
