@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mcmc-iters", type=int, default=21, help="MCMC leg iterations (0 = skip)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
+    ap.add_argument("--no-extra-configs", action="store_true", help="skip the C2/C3 kernel timings")
     return ap.parse_args()
 
 
@@ -297,6 +298,31 @@ def main():
                 "fp64_peak_tflops": FP64_VALU_TFS, "allgather_s": t_ag, "allgather_bytes": gathered_bytes,
                 "allgather_backend": backend if world > 1 else None, "rng": "philox"}
 
+    # ---- the other single-GPU configs of BASELINE.json (C2, C3), kernel time only ----
+    extra = None
+    if world == 1 and not args.no_extra_configs:
+        extra = {}
+        for name, model, method, W in (("C2", "two_i", "dopri5", 65536), ("C3", "chain20", "rk4", 262144),
+                                       ("C3-dopri5", "chain20", "dopri5", 262144)):
+            mx, y0x = build_problem(model, method, T)
+            ex = mx.engine()
+            Sx = len(y0x)
+            thx = torch.as_tensor(synthetic_walkers(W, P), device=dev).contiguous()
+            y0t = torch.as_tensor(np.repeat(y0x[:, None], W, axis=1), device=dev).contiguous()
+            trx = ex.empty_traj(W)
+            ms = []
+            for r in range(7):
+                ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True)
+                if r >= 2:
+                    ms.append(ex.last_kernel_ms())
+            kms = float(np.median(ms))
+            byt = W * (T - 1) * 8 * Sx
+            extra[name] = {"workload": f"{model} {method}, {W} walkers, trajectory mode", "kernel_ms": kms,
+                           "walker_timesteps_per_s": W * (T - 1) / (kms / 1e3),
+                           "hbm_frac": byt / (kms / 1e3) / 1e9 / HBM_PEAK_GBS}
+            del trx, thx, y0t, ex
+            torch.cuda.empty_cache()
+
     if rank == 0:
         line = {
             "metric": "walker-timesteps/sec, 4-state infection ODE, 65536 walkers, 1/2/4/8 MI355X"
@@ -312,6 +338,7 @@ def main():
                          "kernel_ms": kern_avg_s * 1e3, "bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "mcmc": mcmc,
+            "other_configs": extra,
             "chi_finite": chi_ok,
         }
         print(json.dumps(line))

@@ -82,7 +82,9 @@ enum {
   OE_HOST_PTRS = 1u, /* buffers are host memory */
   OE_ASYNC = 2u,     /* do not synchronize before returning (device pointers only) */
   OE_NT_STORES = 4u, /* non-temporal trajectory stores */
-  OE_PIPE = 8u       /* RK4 trajectories via the producer/consumer kernel (opt-in, S <= 8, W even) */
+  OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel (opt-in, S <= 8, W even) */
+  OE_HALF_WAVES = 16u /* RK4: 32 walkers per wavefront (twice the waves; same results). Chosen
+                         automatically for trajectories with S >= 5 at <= 1 wave per SIMD. */
 };
 
 /* RNG modes for oe_mh_run */

@@ -71,6 +71,7 @@ struct CustomModel {
 struct oe_ctx {
   std::vector<std::unique_ptr<CustomModel>> custom;  // user RHS modules (model_id = OE_MODEL_CUSTOM + k)
   std::string arch;
+  int n_cu = 256;
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
@@ -187,6 +188,7 @@ int oe_ctx_create(int32_t device, oe_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
     c->arch = prop.gcnArchName;  // e.g. "gfx950:sramecc+:xnack-"
+    c->n_cu = prop.multiProcessorCount;
   } else {
     c->arch = "gfx950";
   }
@@ -417,7 +419,16 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     const dim3 grid((unsigned)((W + kPipeWalkers - 1) / kPipeWalkers)), block(kPipeThreads);
     e->rk4_piped[nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
   } else {
-    const dim3 grid((unsigned)((W + kBlock - 1) / kBlock)), block(kBlock);
+    // RK4 trajectories of 5+ states at <= 1 wave per SIMD are store-issue bound: run
+    // 32 walkers per wave (twice the storing waves; same bits).  Measured on MI355X at
+    // 65536 walkers: chain5 0.508 -> 0.474 ms, chain6 0.694 -> 0.576, chain8 0.89 ->
+    // 0.77; two_i (4 states) 0.394 vs 0.401, so full waves there.  DOPRI5 keeps 64-lane
+    // groups (its step size is shared per wave).
+    const bool rk4 = c->method == OE_METHOD_RK4;
+    const bool auto_half = rk4 && ia.traj && S >= 5 && W <= (int64_t)64 * 4 * c->n_cu;
+    ia.half = (rk4 && ((flags & OE_HALF_WAVES) || auto_half)) ? 1 : 0;
+    const int64_t per_block = ia.half ? kBlock / 2 : kBlock;
+    const dim3 grid((unsigned)((W + per_block - 1) / per_block)), block(kBlock);
     OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));
   }
   OE_HIP(c, hipGetLastError());

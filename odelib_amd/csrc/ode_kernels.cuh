@@ -122,6 +122,7 @@ __device__ __forceinline__ double pick(const double (&a)[N], int idx) {
 }
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Store one trajectory row element through a buffer resource: descriptor (row base,
 // row bytes) in SGPRs, lane offset w*8 in one VGPR, state offset s*W*8 in an SGPR —
@@ -547,6 +548,7 @@ struct IntegrateArgs {
   double* chi;          // [W] or null
   double* ssres;        // [W] or null
   int32_t* status;      // [W] or null
+  int32_t half;         // 1: 32 walkers per wavefront (lanes 32-63 idle), 0: 64
 };
 
 // parameter registers: the model's own P plus up to 4 '<state>0' initial-condition
@@ -558,9 +560,16 @@ template <class M, int METHOD, bool TRAJ, bool NT>
 __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const IntegrateArgs ia) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
-  const int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = gw < ia.W;
-  const int64_t w = active ? gw : ia.W - 1;  // tail lanes shadow the last walker, never store
+  int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool idle = false;
+  if (ia.half) {  // walker = (wave, lane < 32); the upper half-wave idles (DOPRI5: dead lanes)
+    const int lane = threadIdx.x & 63;
+    gw = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32 + (lane & 31);
+    idle = lane >= 32;
+    if (METHOD == 0 && idle) return;
+  }
+  const bool active = gw < ia.W && !idle;
+  const int64_t w = gw < ia.W ? gw : ia.W - 1;  // tail lanes shadow the last walker, never store
   const int64_t W = ia.W;
   double y[S], p[PMAX];
 #pragma unroll
@@ -601,7 +610,6 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <class M, bool NT>
 __global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevProblem pb, const IntegrateArgs ia) {

@@ -80,6 +80,23 @@ def test_rk4_pipelined_kernel_matches_direct_kernel(spec, W):
         assert np.array_equal(c["traj"].cpu().numpy(), b["traj"].cpu().numpy())
 
 
+@pytest.mark.parametrize("spec", ["two_i", "chain8", "chain20"])
+@pytest.mark.parametrize("W", [1, 33, 4099])
+def test_rk4_half_waves_match_full_waves(spec, W):
+    """32 walkers per wavefront (OE_HALF_WAVES; automatic for S >= 8 trajectories) gives
+    the bits of the 64-walker layout, incl. ragged tails; C restatement as the anchor."""
+    m = _model(spec, "rk4")
+    theta = _walkers(spec, W)
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    eng = m.engine()
+    a = eng.integrate(y0, theta, half_waves=True)
+    b = eng.integrate(y0, theta, trajectory=False)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(a["traj"].cpu().numpy(), ref["traj"])
+    for key in ("chi", "ssres", "status"):
+        assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
+
+
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain8"])
 def test_rk4_substeps_bitwise(spec):
     m = _model(spec, "rk4", substeps=3)

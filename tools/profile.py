@@ -59,7 +59,7 @@ def pmc_pass(out, counter, bench_args, kernel_regex, timeout):
     d = os.path.join(out, f"pmc_{counter.lower()}")
     run(rocprof() + ["--pmc", counter, "--kernel-include-regex", kernel_regex, "--output-format", "csv",
          "-d", d, "-o", "run", "--", sys.executable, "bench.py", "--no-cpu-baseline", "--mcmc-iters", "0",
-         "--steps", "5", "--warmup", "1", *bench_args], timeout)
+         "--no-extra-configs", "--steps", "5", "--warmup", "1", *bench_args], timeout)
     path = find(os.path.join(d, "**", "*counter_collection.csv"))
     rows = read_csv(path)
     vals = {}
@@ -85,7 +85,7 @@ def main():
     # 1. kernel trace + stats (same command line as the bench run, minus the CPU leg)
     d = os.path.join(out, "trace")
     stdout = run(rocprof() + ["--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run", "--",
-                  sys.executable, "bench.py", "--no-cpu-baseline", *bench_args], args.timeout)
+                  sys.executable, "bench.py", "--no-cpu-baseline", "--no-extra-configs", *bench_args], args.timeout)
     bench_line = [l for l in stdout.splitlines() if l.startswith("{")]
     stats_csv = find(os.path.join(d, "**", "*kernel_stats.csv"))
     stats = read_csv(stats_csv)

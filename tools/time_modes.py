@@ -31,16 +31,18 @@ def main():
         y0 = torch.as_tensor(np.repeat(y0h[:, None], W, axis=1), device=dev).contiguous()
         traj = eng.empty_traj(W)
         row = {"case": case}
-        for mode in ("traj", "notraj"):
-            ms = []
-            for r in range(args.reps + 2):
-                if mode == "traj":
-                    eng.integrate(y0, theta, trajectory=True, traj_out=traj, sync=True)
-                else:
-                    eng.integrate(y0, theta, trajectory=False, sync=True)
-                if r >= 2:
-                    ms.append(eng.last_kernel_ms())
-            row[mode + "_ms"] = round(float(np.median(ms)), 4)
+        modes = ("traj", "notraj", "traj_half")
+        ms = {k: [] for k in modes}
+        # interleaved rounds after a warm-up of every mode (clocks settle, pages mapped)
+        for r in range(args.reps + 3):
+            for mode in modes:
+                eng.integrate(y0, theta, trajectory=mode.startswith("traj"),
+                              traj_out=traj if mode.startswith("traj") else None, sync=True,
+                              half_waves=mode.endswith("half"))
+                if r >= 3:
+                    ms[mode].append(eng.last_kernel_ms())
+        for mode in modes:
+            row[mode + "_ms"] = round(float(np.median(ms[mode])), 4)
         row["store_floor_ms"] = round(W * 999 * 8 * S / 6.3e12 * 1e3, 4)
         row["hbm_frac_traj"] = round(W * 999 * 8 * S / (row["traj_ms"] * 1e-3) / 8e12, 4)
         print(json.dumps(row), flush=True)
