@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define OE_ABI_VERSION 1
+#define OE_ABI_VERSION 2
 
 /* return codes */
 enum {
@@ -90,7 +90,11 @@ enum {
 /* RNG modes for oe_mh_run */
 enum {
   OE_RNG_REPLAY = 0, /* caller supplies the proposal increments and uniforms */
-  OE_RNG_PHILOX = 1  /* counter-based Philox4x32-10 keyed by (seed, global walker id) */
+  OE_RNG_PHILOX = 1, /* counter-based Philox4x32-10 keyed by (seed, global walker id) */
+  OE_RNG_NUMPY = 2   /* per chain numpy legacy RandomState(numpy_seeds[w]) on the device, drawn in
+                        the reference's order (Samplers.py:70, 104-127): normal(0, step_sd) per
+                        walking parameter, numpy_prior_draws standard normals (the prior pdf()
+                        calls' lognorm rvs, Framework.py:103), one random_sample() */
 };
 
 typedef struct oe_ctx oe_ctx;
@@ -140,6 +144,10 @@ typedef struct {
   double* final_stats;        /* [4][W] out (may be NULL): chi, rsquared, aic, n_accepted */
   int32_t* status;            /* [W] out (may be NULL): status bits of the integration of the
                                  chain's current (last accepted / initial) state */
+  const uint32_t* numpy_seeds;/* [W] device: per chain seed (NUMPY; MCMC uses the chain index,
+                                 Framework.py:1015/1020) */
+  int32_t numpy_prior_draws;  /* NUMPY: standard normals consumed per iteration after the
+                                 proposal normals */
 } oe_mh_args;
 
 int oe_abi_version(void);
@@ -183,6 +191,14 @@ int oe_integrate(oe_ctx* ctx, int64_t n_walkers, const double* y0, const double*
 
 /* Batched Metropolis–Hastings; device pointers only. */
 int oe_mh_run(oe_ctx* ctx, const oe_mh_args* args, uint32_t flags);
+
+/* The reference's proposal streams on the device: for chain w, numpy legacy
+ * RandomState(seeds[w]) (MT19937, Box–Muller polar gauss with its cached second value,
+ * 53-bit random_sample) consumed per iteration as in OE_RNG_NUMPY.  Writes
+ * dz [nits-1][P][W] (step_sd·N(0,1) for walking parameters, 0 for static ones) and
+ * u [nits-1][W]: the replay_dz / replay_u inputs of OE_RNG_REPLAY.  Device pointers. */
+int oe_numpy_streams(oe_ctx* ctx, int64_t n_walkers, const uint32_t* seeds, int32_t nits, int32_t n_params,
+                     const uint8_t* walk_mask, int32_t prior_draws, double step_sd, double* dz, double* u);
 
 /* Device time (ms) of the kernel launches of the last oe_integrate / oe_mh_run,
  * from HIP events recorded on the context's stream around them (waits for them). */

@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 import pandas as pd
 
-from ..rng import legacy_replay_streams
+from ..rng import device_plan, legacy_replay_streams
 
 
 def lhs_classic(n, samples):
@@ -99,14 +99,22 @@ def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameter
     walk = [p not in reject for p in pnames]
     init_param = [pnames.index(s + "0") if (s + "0") in pnames else -1 for s in snames]
     eng = engine if engine is not None else m0.engine()
-    replay = None
-    if rng == "replay":
+    replay, numpy_seeds, prior_draws = None, None, 0
+    if rng in ("replay", "replay-host"):
+        # the reference's numpy streams: generated on the device when the priors allow
+        # it (rng.device_plan), else on the host ('replay-host' forces the host)
         dists = {p: (m0.parameters[p].dist, m0.parameters[p].hp) for p in pnames}
-        replay = legacy_replay_streams([c.random_seed for c in chains], nits, pnames,
-                                       {p for p in pnames if p not in reject}, dists,
-                                       oldvals=theta.T.tolist())
+        seeds = [c.random_seed for c in chains]
+        walking = {p for p in pnames if p not in reject}
+        plan = device_plan(seeds, pnames, walking, dists, oldvals=theta.T.tolist()) if rng == "replay" else None
+        if plan is not None:
+            rng, numpy_seeds, prior_draws = "numpy", seeds, plan
+        else:
+            rng = "replay"
+            replay = legacy_replay_streams(seeds, nits, pnames, walking, dists, oldvals=theta.T.tolist())
     res = eng.mh_run(theta, y0, nits=nits, burnin=burnin, walk_mask=walk, init_param=init_param, rng=rng,
-                     seed=seed, replay=replay, walker_offset=walker_offset)
+                     seed=seed, replay=replay, walker_offset=walker_offset, numpy_seeds=numpy_seeds,
+                     prior_draws=prior_draws)
     kept = max(0, nits - 1 - burnin)
     if return_device:
         return res

@@ -15,14 +15,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ODELIB_AMD_LIB", os.path.join(_HERE, "csrc", "libodelib_amd.so"))
 
 # --- constants mirrored from include/odelib_amd.h -----------------------------------
-OE_ABI_VERSION = 1
+OE_ABI_VERSION = 2
 OE_OK = 0
 OE_METHOD_RK4, OE_METHOD_DOPRI5 = 0, 1
 OE_MODEL_ZERO_I, OE_MODEL_ONE_I, OE_MODEL_TWO_I, OE_MODEL_CHAIN = 0, 1, 2, 3
 OE_MODEL_CUSTOM = 1000
 OE_STATUS_NONFINITE, OE_STATUS_NEGATIVE, OE_STATUS_MAXSTEP = 1, 2, 4
 OE_HOST_PTRS, OE_ASYNC, OE_NT_STORES, OE_PIPE, OE_HALF_WAVES = 1, 2, 4, 8, 16
-OE_RNG_REPLAY, OE_RNG_PHILOX = 0, 1
+OE_RNG_REPLAY, OE_RNG_PHILOX, OE_RNG_NUMPY = 0, 1, 2
 
 # every symbol include/odelib_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
@@ -38,6 +38,7 @@ EXPORTED = (
     "oe_problem_set",
     "oe_integrate",
     "oe_mh_run",
+    "oe_numpy_streams",
     "oe_last_kernel_ms",
 )
 
@@ -88,6 +89,8 @@ class OEMHArgs(C.Structure):
         ("samples", C.c_void_p),
         ("final_stats", C.c_void_p),
         ("status", C.c_void_p),
+        ("numpy_seeds", C.c_void_p),
+        ("numpy_prior_draws", C.c_int32),
     ]
 
 
@@ -138,6 +141,8 @@ def load_library(path: str | None = None):
         lib.oe_integrate.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, u32]
         lib.oe_mh_run.restype = C.c_int
         lib.oe_mh_run.argtypes = [vp, C.POINTER(OEMHArgs), u32]
+        lib.oe_numpy_streams.restype = C.c_int
+        lib.oe_numpy_streams.argtypes = [vp, i64, vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_double, vp, vp]
         lib.oe_last_kernel_ms.restype = C.c_int
         lib.oe_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
         if lib.oe_abi_version() != OE_ABI_VERSION:
@@ -207,6 +212,10 @@ class Context:
 
     def mh_run(self, args: OEMHArgs, flags=0):
         self._check(self.lib.oe_mh_run(self._h, C.byref(args), int(flags)), "oe_mh_run")
+
+    def numpy_streams(self, n_walkers, seeds, nits, n_params, walk_mask, prior_draws, step_sd, dz, u):
+        self._check(self.lib.oe_numpy_streams(self._h, int(n_walkers), seeds, int(nits), int(n_params), walk_mask,
+                                              int(prior_draws), float(step_sd), dz, u), "oe_numpy_streams")
 
     def last_kernel_ms(self) -> float:
         ms = C.c_double(0.0)

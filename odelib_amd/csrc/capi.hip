@@ -17,6 +17,7 @@
 
 #include "../../include/odelib_amd.h"
 #include "dispatch.h"
+#include "numpy_rng.cuh"
 
 OE_DECLARE_ENTRY(zero_i);
 OE_DECLARE_ENTRY(one_i);
@@ -89,8 +90,10 @@ struct oe_ctx {
   // scratch
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
-  void* draws = nullptr;  // philox proposal draws of one MH chunk
+  void* draws = nullptr;  // philox / numpy proposal draws of one MH chunk
   size_t draws_bytes = 0;
+  void* np_state = nullptr;  // numpy legacy RandomState per chain (key [W][624], pos, gauss, has)
+  size_t np_state_bytes = 0;
 };
 
 namespace {
@@ -136,12 +139,44 @@ int ensure_draws(oe_ctx* c, size_t bytes) {
   return OE_OK;
 }
 
+// per-chain numpy RandomState buffers for W chains
+int ensure_np_state(oe_ctx* c, int64_t W, NpState* st) {
+  const size_t key_b = sizeof(uint32_t) * (size_t)kMtN * (size_t)W;
+  const size_t bytes = key_b + (sizeof(int32_t) * 2 + sizeof(double)) * (size_t)W + 64;
+  if (c->np_state_bytes < bytes) {
+    if (c->np_state) {
+      OE_HIP(c, hipStreamSynchronize(c->stream));
+      OE_HIP(c, hipFree(c->np_state));
+      c->np_state = nullptr;
+      c->np_state_bytes = 0;
+    }
+    OE_HIP(c, hipMalloc(&c->np_state, bytes));
+    c->np_state_bytes = bytes;
+  }
+  char* b = static_cast<char*>(c->np_state);
+  st->key = reinterpret_cast<uint32_t*>(b);
+  st->gauss = reinterpret_cast<double*>(b + key_b);
+  st->pos = reinterpret_cast<int32_t*>(b + key_b + sizeof(double) * (size_t)W);
+  st->has_gauss = st->pos + W;
+  return OE_OK;
+}
+
 int set_device(oe_ctx* c) {
   OE_HIP(c, hipSetDevice(c->device));
   return OE_OK;
 }
 
 }  // namespace
+
+// numpy legacy RandomState per chain: seeding and one chunk of draws (numpy_rng.cuh)
+__global__ void __launch_bounds__(256) k_np_seed(const oe::NpState st, const uint32_t* seeds, int64_t W) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < W) oe::np_seed_lane(st, w, seeds[w]);
+}
+__global__ void __launch_bounds__(256) k_np_draws(const oe::NpDrawArgs d) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < d.W) oe::np_draw_lane(d, w);
+}
 
 // MH proposal draws (philox mode), one lane per walker; see oe::philox_draws
 __global__ void __launch_bounds__(256) k_philox_draws(const oe::DrawArgs d) {
@@ -206,6 +241,7 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->d_rk4) (void)hipFree(c->d_rk4);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->draws) (void)hipFree(c->draws);
+    if (c->np_state) (void)hipFree(c->np_state);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (auto& m : c->custom)
@@ -466,6 +502,9 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   if (a->rng_mode == OE_RNG_REPLAY) {
     if (a->nits > 1 && (!a->replay_dz || !a->replay_u))
       return fail(c, OE_ERR_ARG, "oe_mh_run: replay mode needs replay_dz and replay_u");
+  } else if (a->rng_mode == OE_RNG_NUMPY) {
+    if (!a->numpy_seeds) return fail(c, OE_ERR_ARG, "oe_mh_run: numpy mode needs numpy_seeds");
+    if (a->numpy_prior_draws < 0) return fail(c, OE_ERR_ARG, "oe_mh_run: numpy_prior_draws must be >= 0");
   } else if (a->rng_mode != OE_RNG_PHILOX) {
     return fail(c, OE_ERR_ARG, "oe_mh_run: unknown rng_mode");
   }
@@ -502,30 +541,50 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
 
   const dim3 grid((unsigned)((W + kBlock - 1) / kBlock)), block(kBlock);
   int chunk = a->chunk > 0 ? a->chunk : 25;
-  const bool philox = a->rng_mode == OE_RNG_PHILOX;
+  const bool philox = a->rng_mode == OE_RNG_PHILOX, numpy = a->rng_mode == OE_RNG_NUMPY;
   DrawArgs d{};
-  if (philox && a->nits > 1) {
+  NpDrawArgs nd{};
+  if ((philox || numpy) && a->nits > 1) {
     // one chunk of draws resident at a time, at most ~1 GiB (at least one iteration)
     const size_t per_it = sizeof(double) * (size_t)(P + 1) * (size_t)W;
     chunk = (int)std::max<int64_t>(1, std::min<int64_t>(chunk, (int64_t)((1ull << 30) / per_it)));
     rc = ensure_draws(c, per_it * (size_t)chunk);
     if (rc) return rc;
-    d.W = W;
-    d.walker_offset = a->walker_offset;
-    d.P = P;
-    d.seed_lo = (uint32_t)a->seed;
-    d.seed_hi = (uint32_t)(a->seed >> 32);
-    d.step_sd = a->step_sd;
-    d.dz = static_cast<double*>(c->draws);
-    d.u = d.dz + (size_t)chunk * P * W;
-    m.dz = d.dz;
-    m.u = d.u;
+    double* dz = static_cast<double*>(c->draws);
+    double* u = dz + (size_t)chunk * P * W;
+    m.dz = dz;
+    m.u = u;
+    if (philox) {
+      d.W = W;
+      d.walker_offset = a->walker_offset;
+      d.P = P;
+      d.seed_lo = (uint32_t)a->seed;
+      d.seed_hi = (uint32_t)(a->seed >> 32);
+      d.step_sd = a->step_sd;
+      d.dz = dz;
+      d.u = u;
+    } else {
+      nd.W = W;
+      nd.P = P;
+      nd.prior_draws = a->numpy_prior_draws;
+      nd.zero_static = 0;
+      nd.walk_mask = m.walk_mask;
+      nd.step_sd = a->step_sd;
+      nd.dz = dz;
+      nd.u = u;
+      rc = ensure_np_state(c, W, &nd.st);
+      if (rc) return rc;
+    }
   } else {
     m.dz = a->replay_dz;
     m.u = a->replay_u;
     m.draw_it0 = 1;
   }
   OE_HIP(c, hipEventRecord(c->ev0, c->stream));
+  if (numpy && a->nits > 1) {  // np.random.seed(random_seed), Samplers.py:70
+    hipLaunchKernelGGL(k_np_seed, grid, block, 0, c->stream, nd.st, a->numpy_seeds, W);
+    OE_HIP(c, hipGetLastError());
+  }
   m.init = 1;
   m.it0 = 0;
   m.it1 = 0;
@@ -540,12 +599,55 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       m.draw_it0 = it0;
       hipLaunchKernelGGL(k_philox_draws, grid, block, 0, c->stream, d);
       OE_HIP(c, hipGetLastError());
+    } else if (numpy) {
+      nd.it0 = m.it0;
+      nd.it1 = m.it1;
+      m.draw_it0 = it0;
+      hipLaunchKernelGGL(k_np_draws, grid, block, 0, c->stream, nd);
+      OE_HIP(c, hipGetLastError());
     }
     OE_HIP(c, launch_mh_entry(e, c->method, c->dp, m, grid, block, c->stream));
   }
   OE_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
   if (!(flags & OE_ASYNC)) OE_HIP(c, hipStreamSynchronize(c->stream));
+  return OE_OK;
+}
+
+int oe_numpy_streams(oe_ctx* c, int64_t W, const uint32_t* seeds, int32_t nits, int32_t n_params,
+                     const uint8_t* walk_mask, int32_t prior_draws, double step_sd, double* dz, double* u) {
+  if (!c || !c->own_stream) return OE_ERR_STATE;
+  if (W <= 0 || W > kMaxWalkers) return fail(c, OE_ERR_ARG, "oe_numpy_streams: n_walkers must be in [1, 2^29]");
+  if (nits < 1 || n_params < 1 || n_params > 64 || prior_draws < 0)
+    return fail(c, OE_ERR_ARG, "oe_numpy_streams: need nits >= 1, 1 <= n_params <= 64, prior_draws >= 0");
+  if (!seeds || !walk_mask || (nits > 1 && (!dz || !u)))
+    return fail(c, OE_ERR_ARG, "oe_numpy_streams: seeds, walk_mask, dz and u are required");
+  int rc = set_device(c);
+  if (rc) return rc;
+  if (nits == 1) return OE_OK;
+  NpDrawArgs nd{};
+  nd.W = W;
+  nd.it0 = 1;
+  nd.it1 = nits;
+  nd.P = n_params;
+  nd.prior_draws = prior_draws;
+  nd.zero_static = 1;
+  for (int p = 0; p < n_params; ++p)
+    if (walk_mask[p]) nd.walk_mask |= (1ull << p);
+  nd.step_sd = step_sd;
+  nd.dz = dz;
+  nd.u = u;
+  rc = ensure_np_state(c, W, &nd.st);
+  if (rc) return rc;
+  const dim3 grid((unsigned)((W + kBlock - 1) / kBlock)), block(kBlock);
+  OE_HIP(c, hipEventRecord(c->ev0, c->stream));
+  hipLaunchKernelGGL(k_np_seed, grid, block, 0, c->stream, nd.st, seeds, W);
+  OE_HIP(c, hipGetLastError());
+  hipLaunchKernelGGL(k_np_draws, grid, block, 0, c->stream, nd);
+  OE_HIP(c, hipGetLastError());
+  OE_HIP(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  OE_HIP(c, hipStreamSynchronize(c->stream));
   return OE_OK;
 }
 

@@ -181,14 +181,34 @@ class Engine:
         return self.ctx.last_kernel_ms()
 
     # -- batched Metropolis–Hastings ---------------------------------------------------------
+    def numpy_streams(self, seeds, nits: int, walk_mask, prior_draws: int = 0, step_sd: float = 0.05):
+        """The reference's per-chain numpy legacy draws, generated on the device
+        (``oe_numpy_streams``): dz [nits-1][P][W], u [nits-1][W] — what
+        ``odelib_amd.rng.legacy_replay_streams`` computes on the host."""
+        torch = self.torch
+        P = self.problem.n_params
+        seeds = torch.as_tensor(np.asarray(seeds, dtype=np.int64).astype(np.uint32).view(np.int32),
+                                device=self.dev).contiguous()
+        W = int(seeds.numel())
+        n = max(int(nits) - 1, 0)
+        dz = torch.empty((max(n, 1), P, W), dtype=torch.float64, device=self.dev)
+        u = torch.empty((max(n, 1), W), dtype=torch.float64, device=self.dev)
+        wm = np.ascontiguousarray(np.asarray(walk_mask, dtype=np.uint8).reshape(P))
+        self._sync_stream()
+        self.ctx.numpy_streams(W, seeds.data_ptr(), int(nits), P, wm.ctypes.data, int(prior_draws), float(step_sd),
+                               dz.data_ptr(), u.data_ptr())
+        return dz[:n], u[:n]
+
     def mh_run(self, theta, y0, nits: int, burnin: int, walk_mask, init_param=None, rng: str = "philox",
                seed: int = 0, replay=None, step_sd: float = 0.05, walker_offset: int = 0, chunk: int = 0,
-               sync: bool = True):
+               sync: bool = True, numpy_seeds=None, prior_draws: int = 0):
         """Run W chains; returns dict(samples [kept][P+5][W], theta, y0, final [4][W], status).
 
         rng='replay' takes ``replay=(dz [nits-1][P][W], u [nits-1][W])`` (e.g. from
         ``odelib_amd.rng.legacy_replay_streams``) and reproduces the reference's numpy
-        draws; rng='philox' draws on device, keyed by (seed, walker_offset + w)."""
+        draws; rng='numpy' generates those same draws on the device from ``numpy_seeds``
+        [W] (chain random_seed) with ``prior_draws`` prior normals per iteration;
+        rng='philox' draws on device, keyed by (seed, walker_offset + w)."""
         torch = self.torch
         pb = self.problem
         P, S = pb.n_params, pb.n_states
@@ -226,8 +246,19 @@ class Engine:
             a.replay_u = u.data_ptr() if nits > 1 else None
         elif rng == "philox":
             a.rng_mode = N.OE_RNG_PHILOX
+        elif rng == "numpy":
+            if numpy_seeds is None:
+                raise ValueError("rng='numpy' needs numpy_seeds")
+            sd = torch.as_tensor(np.asarray(numpy_seeds, dtype=np.int64).astype(np.uint32).view(np.int32),
+                                 device=self.dev).contiguous()
+            if sd.numel() != W:
+                raise ValueError("numpy_seeds must have one seed per walker")
+            keep.append(sd)
+            a.rng_mode = N.OE_RNG_NUMPY
+            a.numpy_seeds = sd.data_ptr()
+            a.numpy_prior_draws = int(prior_draws)
         else:
-            raise ValueError("rng must be 'replay' or 'philox'")
+            raise ValueError("rng must be 'replay', 'numpy' or 'philox'")
         a.theta = theta.data_ptr()
         a.y0 = y0.data_ptr()
         a.samples = samples.data_ptr()

@@ -12,7 +12,10 @@ same increments and uniforms as ``Statistics.Samplers.MetropolisHastings``:
     np.random.rand()                                           Samplers.py:127
 
 The prior densities themselves are never used (Samplers.py:118-121), so only the
-draws' consumption is reproduced.  For large ensembles use Philox (rng='philox').
+draws' consumption is reproduced.  ``device_plan`` says when the device generator
+(``oe_numpy_streams`` / rng mode OE_RNG_NUMPY, odelib_amd/csrc/numpy_rng.cuh) can
+produce the same streams: priors that are absent or lognorm (one standard normal per
+rvs) and no falsy old values.  Otherwise this host generator is used.
 """
 from __future__ import annotations
 
@@ -25,6 +28,30 @@ def _consume_rvs(dist, hp, rs):
         rs.standard_normal()
     else:
         dist.rvs(random_state=rs, **(hp or {}))
+
+
+def _is_lognorm(dist):
+    return getattr(getattr(dist, "dist", dist), "name", None) == "lognorm"
+
+
+def device_plan(seeds, pnames, walking, dists, oldvals=None):
+    """Number of prior standard normals per iteration if the device can generate the
+    reference's streams for these chains, else None."""
+    if any(not (0 <= int(s) < 2 ** 32) for s in seeds):
+        return None
+    prior = 0
+    for i, p in enumerate(pnames):
+        if p not in walking:
+            continue
+        d = dists.get(p, (None, None))[0]
+        if d is None:
+            continue
+        if not _is_lognorm(d):
+            return None
+        if oldvals is not None and any(not ov[i] for ov in oldvals):
+            return None  # pdf(oldval) would draw too (Framework.py:99)
+        prior += 1
+    return prior
 
 
 def legacy_replay_streams(seeds, nits, pnames, walking, dists, oldvals=None, step_sd=0.05, shape_dims=None):

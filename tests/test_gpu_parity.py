@@ -366,6 +366,60 @@ def test_dropin_metropolis_hastings_vs_reference_chain(golden, key):
                                    rtol=2e-5, err_msg=c)
 
 
+def _ulps(a, b):
+    a = np.ascontiguousarray(a, dtype=np.float64).view(np.int64)
+    b = np.ascontiguousarray(b, dtype=np.float64).view(np.int64)
+    return np.abs(a - b)
+
+
+def test_device_numpy_streams_match_numpy_legacy():
+    """oe_numpy_streams (MT19937 + polar gauss per chain on the device) gives the
+    reference's draws: uniforms bit-exact (the MT19937 stream and its consumption order
+    are exact), normals within a few ulp in rare draws (the polar method's log is ocml on
+    the device, glibc in numpy)."""
+    import scipy.stats as st
+    from odelib_amd.rng import device_plan, legacy_replay_streams
+    m = _model("two_i", "rk4")
+    pn = m.get_pnames()
+    P = len(pn)
+    W, nits = 257, 140
+    seeds = list(range(W - 1)) + [4000000000]
+    walking = {p for p in pn if p != pn[2]}
+    dists = {p: ((st.lognorm, {"s": 0.5, "scale": 1.0}) if p in pn[:3] else (None, None)) for p in pn}
+    prior = device_plan(seeds, pn, walking, dists)
+    assert prior == 2  # walking lognorm priors: pn[0], pn[1]
+    dz_h, u_h = legacy_replay_streams(seeds, nits, pn, walking, dists)
+    walk = np.array([p in walking for p in pn], np.uint8)
+    dz_d, u_d = m.engine().numpy_streams(seeds, nits, walk, prior_draws=prior)
+    assert np.array_equal(u_d.cpu().numpy(), u_h)
+    d = _ulps(dz_d.cpu().numpy(), dz_h)
+    assert d.max() <= 16 and (d > 0).mean() < 1e-2, (d.max(), (d > 0).mean())
+    assert (dz_d.cpu().numpy()[:, 2, :] == 0).all()
+
+
+@pytest.mark.parametrize("method", ["rk4", "dopri5"])
+def test_mh_device_numpy_rng_equals_host_replay(method):
+    """rng='numpy' (draws generated on the device per chunk) runs the same chains as
+    rng='replay' fed with the host numpy streams."""
+    import scipy.stats as st
+    from odelib_amd.rng import legacy_replay_streams
+    m, P, theta, y0 = _mh_inputs("two_i", 200, method)
+    pn = m.get_pnames()
+    walk = np.ones(P, np.uint8)
+    walk[3] = 0
+    walking = {p for j, p in enumerate(pn) if walk[j]}
+    dists = {p: (st.lognorm, {"s": 1.0, "scale": 1.0}) for p in pn}
+    seeds = np.arange(200) * 7 + 3
+    nits = 60
+    eng = m.engine()
+    host = eng.mh_run(theta, y0, nits=nits, burnin=20, walk_mask=walk, rng="replay",
+                      replay=legacy_replay_streams(seeds, nits, pn, walking, dists), chunk=7)
+    dev = eng.mh_run(theta, y0, nits=nits, burnin=20, walk_mask=walk, rng="numpy", numpy_seeds=seeds,
+                     prior_draws=len(walking), chunk=7)
+    for k in ("samples", "theta", "final"):
+        np.testing.assert_allclose(dev[k].cpu().numpy(), host[k].cpu().numpy(), rtol=1e-12, err_msg=k)
+
+
 def test_dropin_mcmc_vs_reference(golden, capsys):
     meta = golden.meta["mcmc"]
     m = product_model("one_i", rtol=1e-10, atol=1e-10)

@@ -180,3 +180,62 @@ def test_compute_without_gpu_fails_loudly():
         m.integrate()
     with pytest.raises(N.NativeUnavailable):
         m.MCMC(chain_inits=[THETA["two_i"]], iterations_per_chain=4, print_report=False)
+
+
+def test_lazy_mt19937_twist_and_polar_gauss_reproduce_numpy_legacy_stream():
+    """The device generator's algorithm (odelib_amd/csrc/numpy_rng.cuh: init_genrand,
+    one-word-per-draw lazy twist, 53-bit doubles, polar gauss with its cached value),
+    restated in Python, reproduces numpy's legacy RandomState bit for bit."""
+    import math
+
+    def stream(seed, n_gauss, n_dbl):
+        key = [0] * 624
+        s = seed
+        for i in range(624):
+            key[i] = s
+            s = (1812433253 * (s ^ (s >> 30)) + i + 1) & 0xFFFFFFFF
+        st = {"pos": 0, "has": False, "g": 0.0}
+
+        def next32():
+            i = st["pos"]
+            i1 = 0 if i + 1 == 624 else i + 1
+            im = i + 397 - 624 if i + 397 >= 624 else i + 397
+            y = (key[i] & 0x80000000) | (key[i1] & 0x7FFFFFFF)
+            v = key[im] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+            key[i] = v
+            st["pos"] = i1
+            t = v ^ (v >> 11)
+            t ^= (t << 7) & 0x9D2C5680
+            t ^= (t << 15) & 0xEFC60000
+            return t ^ (t >> 18)
+
+        def dbl():
+            a, b = next32() >> 5, next32() >> 6
+            return (a * 67108864.0 + b) / 9007199254740992.0
+
+        def gauss():
+            if st["has"]:
+                st["has"] = False
+                return st["g"]
+            while True:
+                x1 = 2.0 * dbl() - 1.0
+                x2 = 2.0 * dbl() - 1.0
+                r2 = x1 * x1 + x2 * x2
+                if r2 < 1.0 and r2 != 0.0:
+                    break
+            f = math.sqrt(-2.0 * math.log(r2) / r2)
+            st["g"], st["has"] = f * x1, True
+            return f * x2
+
+        out = []
+        for _ in range(n_gauss):
+            out.append(gauss())
+        for _ in range(n_dbl):
+            out.append(dbl())
+        return out
+
+    for seed in (0, 1, 7, 123456789):
+        rs = np.random.RandomState(seed)
+        want = [rs.standard_normal() for _ in range(701)] + [rs.rand() for _ in range(650)]
+        got = stream(seed, 701, 650)
+        assert got == want, seed
