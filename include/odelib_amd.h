@@ -140,7 +140,8 @@ typedef struct {
   double* theta;              /* [P][W] in: initial θ; out: final θ */
   double* y0;                 /* [S][W] in: initial states; out: final states */
   double* samples;            /* [nits-1-burnin][P+5][W] out: θ, chi, rsquared, aic,
-                                 iteration, acceptance_ratio (Samplers.py:160-165) */
+                                 iteration, acceptance_ratio (Samplers.py:160-165)
+                                 (resume: [nits-max(it_start, burnin+1)][P+5][W]) */
   double* final_stats;        /* [4][W] out (may be NULL): chi, rsquared, aic, n_accepted */
   int32_t* status;            /* [W] out (may be NULL): status bits of the integration of the
                                  chain's current (last accepted / initial) state */
@@ -148,6 +149,13 @@ typedef struct {
                                  Framework.py:1015/1020) */
   int32_t numpy_prior_draws;  /* NUMPY: standard normals consumed per iteration after the
                                  proposal normals */
+  int32_t it_start;           /* 0 or 1: fresh run (a-priori fit first, Samplers.py:88-91).
+                                 k > 1: RESUME at reference iteration k from a checkpoint:
+                                 theta, y0, final_stats and status hold the chain state after
+                                 iteration k-1 (inputs); samples receives the rows of iterations
+                                 max(k, burnin+1)..nits-1.  Philox counters and replay arrays
+                                 are indexed by iteration; NUMPY streams are re-seeded and
+                                 fast-forwarded on the device.  Same results as one run. */
 } oe_mh_args;
 
 int oe_abi_version(void);

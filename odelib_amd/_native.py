@@ -91,6 +91,7 @@ class OEMHArgs(C.Structure):
         ("status", C.c_void_p),
         ("numpy_seeds", C.c_void_p),
         ("numpy_prior_draws", C.c_int32),
+        ("it_start", C.c_int32),
     ]
 
 

@@ -1,0 +1,34 @@
+"""Checkpoint / resume of device MCMC chains ("persist θ, chi and the RNG
+counter per walker").
+
+The chain state after iteration k-1 is θ [P][W], the current states y0 [S][W], the
+running (chi, rsquared, aic, n_accepted) [4][W] and the status word [W]; the random
+streams are a function of the iteration (Philox counters, replay arrays) or are
+re-seeded and fast-forwarded on the device (numpy legacy streams), so nothing else is
+needed.  ``Engine.mh_run(..., resume=load(path))`` continues with the draws an
+uninterrupted run would have used.  Files are plain ``.npz`` (no pickles).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+_KEYS = ("theta", "y0", "final", "status")
+
+
+def save(path, result, meta=None):
+    """Write the chain state of an ``Engine.mh_run`` result (+ JSON-able ``meta``)."""
+    import json
+    arrays = {k: (result[k].cpu().numpy() if hasattr(result[k], "cpu") else np.asarray(result[k])) for k in _KEYS}
+    arrays["next_it"] = np.asarray(int(result["next_it"]), np.int64)
+    arrays["meta"] = np.asarray(json.dumps(meta or {}))
+    np.savez(path, **arrays)
+
+
+def load(path):
+    """Chain state written by ``save``: dict(theta, y0, final, status, next_it, meta)."""
+    import json
+    with np.load(path, allow_pickle=False) as z:
+        out = {k: z[k] for k in _KEYS}
+        out["next_it"] = int(z["next_it"])
+        out["meta"] = json.loads(str(z["meta"]))
+    return out

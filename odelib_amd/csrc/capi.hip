@@ -497,7 +497,12 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   if (a->burnin < 0) return fail(c, OE_ERR_ARG, "oe_mh_run: burnin must be >= 0");
   if (!a->theta || !a->y0 || !a->walk_mask || !a->init_param)
     return fail(c, OE_ERR_ARG, "oe_mh_run: theta, y0, walk_mask and init_param are required");
-  const int kept = std::max(0, a->nits - 1 - a->burnin);
+  const int it_start = a->it_start > 1 ? a->it_start : 1;
+  const bool resume = it_start > 1;
+  if (resume && (it_start > a->nits || !a->final_stats))
+    return fail(c, OE_ERR_ARG, "oe_mh_run: resume needs it_start <= nits and the chain state in final_stats");
+  const int row0 = std::max(it_start, a->burnin + 1);
+  const int kept = std::max(0, a->nits - row0);
   if (kept > 0 && !a->samples) return fail(c, OE_ERR_ARG, "oe_mh_run: samples buffer required");
   if (a->rng_mode == OE_RNG_REPLAY) {
     if (a->nits > 1 && (!a->replay_dz || !a->replay_u))
@@ -516,6 +521,7 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   m.W = W;
   m.walker_offset = a->walker_offset;
   m.burnin = a->burnin;
+  m.row0 = row0;
   m.walk_mask = 0;
   for (int p = 0; p < P; ++p)
     if (a->walk_mask[p]) m.walk_mask |= (1ull << p);
@@ -584,13 +590,21 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   if (numpy && a->nits > 1) {  // np.random.seed(random_seed), Samplers.py:70
     hipLaunchKernelGGL(k_np_seed, grid, block, 0, c->stream, nd.st, a->numpy_seeds, W);
     OE_HIP(c, hipGetLastError());
+    for (int f0 = 1; f0 < it_start; f0 += chunk) {  // resume: replay the consumed draws
+      nd.it0 = f0;
+      nd.it1 = std::min(it_start, f0 + chunk);
+      hipLaunchKernelGGL(k_np_draws, grid, block, 0, c->stream, nd);
+      OE_HIP(c, hipGetLastError());
+    }
   }
-  m.init = 1;
-  m.it0 = 0;
-  m.it1 = 0;
-  OE_HIP(c, launch_mh_entry(e, c->method, c->dp, m, grid, block, c->stream));
+  if (!resume) {
+    m.init = 1;
+    m.it0 = 0;
+    m.it1 = 0;
+    OE_HIP(c, launch_mh_entry(e, c->method, c->dp, m, grid, block, c->stream));
+  }
   m.init = 0;
-  for (int it0 = 1; it0 < a->nits; it0 += chunk) {
+  for (int it0 = it_start; it0 < a->nits; it0 += chunk) {
     m.it0 = it0;
     m.it1 = std::min(a->nits, it0 + chunk);
     if (philox) {

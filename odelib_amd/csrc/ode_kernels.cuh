@@ -785,6 +785,7 @@ struct MHArgs {
   int64_t walker_offset;
   int32_t it0, it1;        // iteration range of this launch (1-based, ref `it`)
   int32_t burnin;
+  int32_t row0;            // iteration stored in samples row 0 (burnin+1, or later on resume)
   int32_t draw_it0;        // iteration whose draws sit at offset 0 of dz/u
   int32_t init;            // 1: compute the a-priori chi/R²/AIC only (Samplers.py:88-91)
   int32_t any_walk;
@@ -879,7 +880,7 @@ __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma
     }
     // ---- keep the sample after burn-in (Samplers.py:147-153)
     if (it > ma.burnin && active) {
-      double* row = ma.samples + (int64_t)(it - ma.burnin - 1) * PS * W + w;
+      double* row = ma.samples + (int64_t)(it - ma.row0) * PS * W + w;
 #pragma unroll
       for (int j = 0; j < PMAX; ++j)
         if (j < P) row[(int64_t)j * W] = th[j];

@@ -201,26 +201,42 @@ class Engine:
 
     def mh_run(self, theta, y0, nits: int, burnin: int, walk_mask, init_param=None, rng: str = "philox",
                seed: int = 0, replay=None, step_sd: float = 0.05, walker_offset: int = 0, chunk: int = 0,
-               sync: bool = True, numpy_seeds=None, prior_draws: int = 0):
+               sync: bool = True, numpy_seeds=None, prior_draws: int = 0, resume=None):
         """Run W chains; returns dict(samples [kept][P+5][W], theta, y0, final [4][W], status).
 
         rng='replay' takes ``replay=(dz [nits-1][P][W], u [nits-1][W])`` (e.g. from
         ``odelib_amd.rng.legacy_replay_streams``) and reproduces the reference's numpy
         draws; rng='numpy' generates those same draws on the device from ``numpy_seeds``
         [W] (chain random_seed) with ``prior_draws`` prior normals per iteration;
-        rng='philox' draws on device, keyed by (seed, walker_offset + w)."""
+        rng='philox' draws on device, keyed by (seed, walker_offset + w).
+
+        ``resume`` continues a previous run's chains (a result dict of this method, or
+        one loaded by ``odelib_amd.checkpoint.load``): its theta, y0, final and status
+        are the chain state after iteration ``resume['next_it'] - 1``; iterations
+        next_it..nits-1 run with the same draws as one uninterrupted run, and samples
+        holds the kept rows from max(next_it, burnin+1) on."""
         torch = self.torch
         pb = self.problem
         P, S = pb.n_params, pb.n_states
+        nits = int(nits)
+        burnin = int(burnin)
+        it_start = 1
+        if resume is not None:
+            it_start = int(resume["next_it"])
+            theta, y0 = resume["theta"], resume["y0"]
         W = int((theta if isinstance(theta, torch.Tensor) else np.asarray(theta)).shape[1])
         theta = self._dev(theta, (P, W)).clone()
         y0 = self._dev(y0, (S, W)).clone()
-        nits = int(nits)
-        burnin = int(burnin)
-        kept = max(0, nits - 1 - burnin)
+        kept = max(0, nits - max(it_start, burnin + 1))
         samples = torch.empty((max(kept, 1), P + 5, W), dtype=torch.float64, device=self.dev)
-        final = torch.empty((4, W), dtype=torch.float64, device=self.dev)
-        status = torch.zeros(W, dtype=torch.int32, device=self.dev)
+        if resume is not None:
+            final = self._dev(resume["final"], (4, W)).clone()
+            st = resume["status"]
+            status = (st if isinstance(st, torch.Tensor) else torch.as_tensor(np.asarray(st, np.int32))).to(
+                device=self.dev, dtype=torch.int32).clone()
+        else:
+            final = torch.empty((4, W), dtype=torch.float64, device=self.dev)
+            status = torch.zeros(W, dtype=torch.int32, device=self.dev)
         wm = np.ascontiguousarray(np.asarray(walk_mask, dtype=np.uint8).reshape(P))
         ip = np.full(S, -1, np.int32) if init_param is None else np.ascontiguousarray(
             np.asarray(init_param, dtype=np.int32).reshape(S))
@@ -229,6 +245,7 @@ class Engine:
         a.walker_offset = int(walker_offset)
         a.nits = nits
         a.burnin = burnin
+        a.it_start = it_start
         a.chunk = int(chunk)
         a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         a.step_sd = float(step_sd)
@@ -238,8 +255,9 @@ class Engine:
         if rng == "replay":
             if replay is None:
                 raise ValueError("rng='replay' needs replay=(dz, u)")
-            dz = self._dev(replay[0], (max(nits - 1, 0), P, W))
-            u = self._dev(replay[1], (max(nits - 1, 0), W))
+            n = max(nits - 1, 0)  # streams may be longer (a run stopped early for a checkpoint)
+            dz = self._dev(replay[0][:n], (n, P, W))
+            u = self._dev(replay[1][:n], (n, W))
             keep += [dz, u]
             a.rng_mode = N.OE_RNG_REPLAY
             a.replay_dz = dz.data_ptr() if nits > 1 else None
@@ -269,7 +287,7 @@ class Engine:
         if sync:
             torch.cuda.synchronize(self.dev)
         return {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status,
-                "_keep": keep}
+                "next_it": max(nits, it_start), "_keep": keep}
 
     def close(self):
         self.ctx.close()

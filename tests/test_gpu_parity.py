@@ -420,6 +420,38 @@ def test_mh_device_numpy_rng_equals_host_replay(method):
         np.testing.assert_allclose(dev[k].cpu().numpy(), host[k].cpu().numpy(), rtol=1e-12, err_msg=k)
 
 
+@pytest.mark.parametrize("rng", ["philox", "numpy", "replay"])
+@pytest.mark.parametrize("split", [5, 17, 40])
+def test_mh_checkpoint_resume_equals_one_run(tmp_path, rng, split):
+    """Stop after iteration split-1, checkpoint to disk, resume to nits: the same chains,
+    samples and final state as one uninterrupted run (split before / after burn-in)."""
+    from odelib_amd import checkpoint
+    from odelib_amd.rng import legacy_replay_streams
+    import scipy.stats as st
+    m, P, theta, y0 = _mh_inputs("two_i", 130, "rk4")
+    pn = m.get_pnames()
+    walk = np.ones(P, np.uint8)
+    nits, burnin = 50, 25
+    seeds = np.arange(130)
+    kw = dict(walk_mask=walk, rng=rng, seed=11, numpy_seeds=seeds, prior_draws=P, chunk=6)
+    if rng == "replay":
+        kw["replay"] = legacy_replay_streams(seeds, nits, pn, set(pn), {p: (st.lognorm, {"s": 1}) for p in pn})
+    eng = m.engine()
+    full = eng.mh_run(theta, y0, nits=nits, burnin=burnin, **kw)
+    part = eng.mh_run(theta, y0, nits=split, burnin=burnin, **kw)
+    path = tmp_path / "chains.npz"
+    checkpoint.save(path, part, meta={"rng": rng})
+    rest = eng.mh_run(None, None, nits=nits, burnin=burnin, resume=checkpoint.load(path), **kw)
+    for k in ("theta", "y0", "final", "status"):
+        assert np.array_equal(rest[k].cpu().numpy(), full[k].cpu().numpy()), k
+    s_full = full["samples"].cpu().numpy()
+    s_rest = rest["samples"].cpu().numpy()
+    first = max(split, burnin + 1)
+    assert np.array_equal(s_rest, s_full[first - burnin - 1:])
+    if split > burnin + 1:
+        assert np.array_equal(part["samples"].cpu().numpy(), s_full[:split - burnin - 1])
+
+
 def test_dropin_mcmc_vs_reference(golden, capsys):
     meta = golden.meta["mcmc"]
     m = product_model("one_i", rtol=1e-10, atol=1e-10)

@@ -239,3 +239,15 @@ def test_lazy_mt19937_twist_and_polar_gauss_reproduce_numpy_legacy_stream():
         want = [rs.standard_normal() for _ in range(701)] + [rs.rand() for _ in range(650)]
         got = stream(seed, 701, 650)
         assert got == want, seed
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    from odelib_amd import checkpoint
+    rs = np.random.RandomState(3)
+    res = {"theta": rs.rand(5, 7), "y0": rs.rand(4, 7), "final": rs.rand(4, 7),
+           "status": np.arange(7, dtype=np.int32), "next_it": 12}
+    checkpoint.save(tmp_path / "c.npz", res, meta={"seed": 3})
+    back = checkpoint.load(tmp_path / "c.npz")
+    for k in ("theta", "y0", "final", "status"):
+        assert np.array_equal(back[k], res[k])
+    assert back["next_it"] == 12 and back["meta"] == {"seed": 3}
