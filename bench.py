@@ -297,13 +297,21 @@ def main():
         eng.mh_run(theta, y0, nits=nits, burnin=burn, walk_mask=walk, rng="numpy", numpy_seeds=seeds,
                    prior_draws=P)
         np_kernel_ms = eng.last_kernel_ms()
+        # Fitting-report statistics of the pooled posterior (rawstats, Framework.py:11-17)
+        # from two all-reduces of per-parameter sufficient statistics
+        from odelib_amd.distributed import pooled_rawstats
+        torch.cuda.synchronize(dev)
+        tr0 = time.perf_counter()
+        med, _ = pooled_rawstats(r["samples"], P)
+        t_rs = time.perf_counter() - tr0
         mh_wts = n_gpus * Wl * (T - 1) * nits  # a-priori integrate + nits-1 proposals
         flops_per_wts = 4 * 20 + 4 * 12  # 4 RHS x ~20 flop + RK update (4-state two_i)
         mcmc = {"iterations": nits, "walker_timesteps_per_s": mh_wts / t_mh, "kernel_ms": mh_kernel_ms,
                 "fp64_tflops_est": Wl * (T - 1) * nits * flops_per_wts * (S / 4.0) / (mh_kernel_ms / 1e3) / 1e12,
                 "fp64_peak_tflops": FP64_VALU_TFS, "allgather_s": t_ag, "allgather_bytes": gathered_bytes,
                 "allgather_backend": backend if world > 1 else None, "rng": "philox",
-                "kernel_ms_numpy_rng": np_kernel_ms}
+                "kernel_ms_numpy_rng": np_kernel_ms, "rawstats_allreduce_s": t_rs,
+                "posterior_median": [float(x) for x in med]}
 
     # ---- the other single-GPU configs of BASELINE.json (C2, C3), kernel time only ----
     extra = None

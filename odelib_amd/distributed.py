@@ -64,3 +64,31 @@ def sharded_mh(engine, theta_all, y0_all, nits: int, burnin: int, walk_mask, ini
                       walk_mask=walk_mask, init_param=init_param, rng="philox", seed=seed, step_sd=step_sd,
                       walker_offset=off)
     return allgather_walkers(r["samples"], W, group=group), r
+
+
+def pooled_rawstats(block, n_params: int, group=None):
+    """``rawstats`` (Framework.py:11-17: median = exp(mean log x), log-normal std from the
+    ddof=1 std of log x) of every parameter over the POOLED posterior, from the per-rank
+    sample blocks [kept][P+5][count_r] without gathering them: two all-reduces of
+    per-parameter sufficient statistics (n, Σ log x, then Σ (log x − mean)²), 2P+1 and P
+    doubles.  Without an initialised process group it is the single-process result.
+    Returns (median [P], std [P]) as numpy arrays."""
+    import torch
+    import torch.distributed as dist
+    dist_on = dist.is_available() and dist.is_initialized()
+    P = int(n_params)
+    lx = torch.log(block[:, :P, :].to(torch.float64)).permute(1, 0, 2).reshape(P, -1)  # [P][kept*count]
+    dev = lx.device if (not dist_on or dist.get_backend(group) == "nccl") else torch.device("cpu")
+    s1 = torch.cat([lx.sum(dim=1), torch.tensor([float(lx.shape[1])], dtype=torch.float64, device=lx.device)]).to(dev)
+    if dist_on:
+        dist.all_reduce(s1, group=group)
+    n = s1[P]
+    mean = s1[:P] / n
+    s2 = ((lx - mean.to(lx.device)[:, None]) ** 2).sum(dim=1).to(dev)
+    if dist_on:
+        dist.all_reduce(s2, group=group)
+    var = s2 / (n - 1.0)
+    mean, var = mean.cpu().numpy(), var.cpu().numpy()
+    median = np.exp(mean)
+    std = ((np.exp(var) - 1) * np.exp(2 * mean + var)) ** 0.5
+    return median, std

@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from odelib_amd.distributed import allgather_walkers, shard, sharded_mh
+from odelib_amd.distributed import allgather_walkers, pooled_rawstats, shard, sharded_mh
 
 
 def test_shard_partitions():
@@ -63,8 +63,12 @@ def _worker(rank, world, port, W, q):
         y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
         pooled, _ = sharded_mh(_OracleEngine(fp), theta, y0, nits=6, burnin=2, walk_mask=np.ones(P, np.uint8),
                                seed=11)
+        # 3. rawstats of the pooled posterior from all-reduced sufficient statistics
+        off, cnt = shard(W, rank, world)
+        med, sd = pooled_rawstats(pooled[..., off:off + cnt], P)
         if rank == 0:
             q.put(pooled.numpy())
+            q.put((med, sd))
     finally:
         dist.destroy_process_group()
 
@@ -79,6 +83,7 @@ def test_gloo_world2_sharded_mh_matches_single_process():
     for p in procs:
         p.start()
     pooled = q.get(timeout=240)
+    med, sd = q.get(timeout=60)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -89,3 +94,8 @@ def test_gloo_world2_sharded_mh_matches_single_process():
     y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
     ref = rk_ref.mh_run(m.fit_problem(), theta, y0, 6, 2, np.ones(5, np.uint8), rng="philox", seed=11)
     assert np.array_equal(pooled, ref["samples"])
+    import pandas as pd
+    from odelib_amd.Framework import rawstats
+    for j in range(5):  # Framework.py:11-17 on the concatenated posterior column
+        m_ref, s_ref = rawstats(pd.Series(pooled[:, j, :].reshape(-1)))
+        np.testing.assert_allclose([med[j], sd[j]], [m_ref, s_ref], rtol=1e-12)
