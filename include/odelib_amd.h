@@ -83,8 +83,10 @@ enum {
   OE_ASYNC = 2u,     /* do not synchronize before returning (device pointers only) */
   OE_NT_STORES = 4u, /* non-temporal trajectory stores */
   OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel (opt-in, S <= 8, W even) */
-  OE_HALF_WAVES = 16u /* RK4: 32 walkers per wavefront (twice the waves; same results). Chosen
+  OE_HALF_WAVES = 16u, /* RK4: 32 walkers per wavefront (twice the waves; same results). Chosen
                          automatically for trajectories with S >= 5 at <= 1 wave per SIMD. */
+  OE_SPLIT_WAVES = 32u /* trajectories: two wavefronts integrate the same 64 walkers and each
+                          stores half of the states (twice the storing waves; same results) */
 };
 
 /* RNG modes for oe_mh_run */

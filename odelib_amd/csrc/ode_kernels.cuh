@@ -142,16 +142,27 @@ __device__ __forceinline__ void check_finite(const double (&y)[S], Acc& a) {
 // Store grid row i of the trajectory (TRAJ) and track the minimum state.  `off` is
 // the lane's byte offset w*8 (32-bit); rows are stored through a per-row buffer
 // descriptor (S*W*8 < 2^32, checked on the host): no per-store VALU address math.
+// `sp` (wave-uniform) selects the states this wave stores: -1 all of them; with split
+// waves (two waves integrate the same 64 walkers) 0 the lower half [0, S/2), 1 the upper.
 template <int S, bool TRAJ, bool NT>
 __device__ __forceinline__ void store_row(int i, const double (&y)[S], double* __restrict__ traj,
-                                          int64_t W, uint32_t off, bool active, Acc& a) {
+                                          int64_t W, uint32_t off, bool active, Acc& a, int sp) {
   if constexpr (TRAJ) {
     if (active) {
       const uint32_t row_bytes = (uint32_t)(S * W * 8);
       const __amdgpu_buffer_rsrc_t rsrc =
           __builtin_amdgcn_make_buffer_rsrc((void*)(traj + (int64_t)i * S * W), 0, row_bytes, 0x00020000);
+      constexpr int H = S / 2;
+      if (sp < 0) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
+        for (int s = 0; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
+      } else if (sp == 0) {
+#pragma unroll
+        for (int s = 0; s < H; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
+      } else {
+#pragma unroll
+        for (int s = H; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
+      }
     }
   }
 #pragma unroll
@@ -199,8 +210,8 @@ __device__ __forceinline__ void observe_next(const DevProblem& pb, int i, const 
 template <int S, bool TRAJ, bool NT>
 __device__ __forceinline__ void emit(const DevProblem& pb, int i, const double (&y)[S],
                                      double* __restrict__ traj, int64_t W, uint32_t off,
-                                     bool active, int& k, Acc& a) {
-  store_row<S, TRAJ, NT>(i, y, traj, W, off, active, a);
+                                     bool active, int& k, Acc& a, int sp) {
+  store_row<S, TRAJ, NT>(i, y, traj, W, off, active, a, sp);
   observe<S>(pb, i, y, k, a);
 }
 
@@ -240,18 +251,23 @@ __device__ __forceinline__ void rk4_step(double (&y)[M::S], double t, double h, 
 template <class M, int PMAX, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[M::S],
                                               const double (&p)[PMAX], double* traj,
-                                              int64_t W, uint32_t off, bool active, Acc& a) {
+                                              int64_t W, uint32_t off, bool active, Acc& a, int sp) {
   int k = 0;
-  emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
+  emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a, sp);
   const int n = pb.substeps;
   const cptr<double> tab = kconst(pb.rk4);
   const cptr<Obs> obs = kconst(pb.obs);
-  // one output interval: per-interval constants computed on the host exactly as
-  // h = (t_i - t_{i-1}) / n, hh = 0.5*h, h6 = h/6; substep j starts at t_{i-1} + j*h
+  // Per-interval constants computed on the host exactly as h = (t_i - t_{i-1}) / n,
+  // hh = 0.5*h, h6 = h/6, t_{i-1}; substep j starts at t_{i-1} + j*h.  The NEXT
+  // interval's row is loaded while this interval computes: a lone wave otherwise waits
+  // out a scalar-cache miss (one 64-B line per two intervals) every other step.
+  double h = tab[0], hh = tab[1], h6 = tab[2], t = tab[3];
+  const int last_row = pb.T - 2;
   auto interval = [&](int i) {
-    const double h = tab[4 * (i - 1)], hh = tab[4 * (i - 1) + 1], h6 = tab[4 * (i - 1) + 2];
-    const double t = tab[4 * (i - 1) + 3];
+    const int nx = i < last_row ? i : last_row;  // table row of interval i+1 (clamped)
+    const double hn = tab[4 * nx], hhn = tab[4 * nx + 1], h6n = tab[4 * nx + 2], tn = tab[4 * nx + 3];
     for (int j = 0; j < n; ++j) rk4_step<M, PMAX>(y, t + (double)j * h, h, hh, h6, p);
+    h = hn; hh = hhn; h6 = h6n; t = tn;
   };
   int i = 1;
   while (i < pb.T) {
@@ -259,11 +275,11 @@ __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[
     const int next = (k < pb.n_obs) ? obs[k].tidx : pb.T;
     for (; i < next; ++i) {
       interval(i);
-      if constexpr (TRAJ) store_row<M::S, TRAJ, NT>(i, y, traj, W, off, active, a);
+      if constexpr (TRAJ) store_row<M::S, TRAJ, NT>(i, y, traj, W, off, active, a, sp);
     }
     if (i < pb.T) {  // i == next: an observed grid point
       interval(i);
-      emit<M::S, TRAJ, NT>(pb, i, y, traj, W, off, active, k, a);
+      emit<M::S, TRAJ, NT>(pb, i, y, traj, W, off, active, k, a, sp);
       ++i;
     }
   }
@@ -322,11 +338,11 @@ __device__ __forceinline__ double inv_fifth_root(double x) {
 template <class M, int PMAX, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
-                                                 int64_t W, uint32_t off, bool active, Acc& a) {
+                                                 int64_t W, uint32_t off, bool active, Acc& a, int sp) {
   using namespace dp;
   constexpr int S = M::S;
   int k = 0;
-  emit<S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
+  emit<S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a, sp);
   const cptr<double> times = kconst(pb.times);
   const double t0 = times[0];
   const double tend = times[pb.T - 1];
@@ -428,14 +444,27 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 
     if (err <= 1.0) {
       const double tn = last ? tend : t + h;
-      // dense output for every grid point in (t, tn]; for small S Hairer's coefficients
-      // are formed once per step (on the first grid point that needs them), for large S
-      // per grid point (four more S-vectors would spill)
-      constexpr bool kHoist = S <= 8;
+      // Dense output for every grid point in (t, tn] from Hairer's coefficients
+      // ydf, bsp, r4, r5.  Trajectory mode: formed eagerly once per accepted step (a grid
+      // point nearly always falls in the step, and k2..k6 die before the output loop).
+      // Otherwise (observed points only): small S forms them on the first observed point
+      // of the step, large S per observed point (lazily kept k's would spill).
+      constexpr bool kEager = TRAJ;
+      constexpr bool kHoist = TRAJ || S <= 8;
       bool have_dense = false;
       const double rh = 1.0 / h;  // one division per step, not per grid point
       double ydf[kHoist ? S : 1], bsp[kHoist ? S : 1], r4[kHoist ? S : 1], r5[kHoist ? S : 1];
       const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
+      if constexpr (kEager) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          ydf[s] = yn[s] - y[s];
+          bsp[s] = fma(h, k1[s], -ydf[s]);
+          r4[s] = fma(-h, k7[s], ydf[s]) - bsp[s];
+          r5[s] = fma(hd7, k7[s], fma(hd6, k6[s], fma(hd5, k5[s], fma(hd4, k4[s], fma(hd3, k3[s], hd1 * k1[s])))));
+        }
+        have_dense = true;
+      }
       while (i < pb.T && (kLean ? times[i] : t_i) <= tn) {
         const double ti = kLean ? times[i] : t_i;
         if constexpr (!kLean) t_i = times[i + 1 < pb.T ? i + 1 : i];  // issued now, used next iteration
@@ -448,7 +477,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
             const double th = (ti - t) * rh;
             const double th1 = 1.0 - th;
             if constexpr (kHoist) {
-              if (!have_dense) {
+              if (!kEager && !have_dense) {
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                   ydf[s] = yn[s] - y[s];
@@ -477,10 +506,10 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
               for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
             }
-            emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
+            emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a, sp);
           } else {
             // (an evicted lane's state is NaN, so its dense output is NaN already)
-            store_row<S, TRAJ, NT>(i, yo, traj, W, off, active, a);
+            store_row<S, TRAJ, NT>(i, yo, traj, W, off, active, a, sp);
             observe_next<S>(pb, i, yo, k, nxt, a);
           }
         }
@@ -517,7 +546,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
         for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
         for (; i < pb.T; ++i)
-          if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
+          if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a, sp);
         break;
       }
       if (h < hmin) h = fmin(1e-3 * span, tend - t);
@@ -531,10 +560,10 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 template <class M, int PMAX, int METHOD, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
-                                                 int64_t W, int64_t w, bool active, Acc& a) {
+                                                 int64_t W, int64_t w, bool active, Acc& a, int sp = -1) {
   const uint32_t off = (uint32_t)w * 8u;  // byte offset of walker w in a [..][W] row
-  if constexpr (METHOD == 0) integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
-  else integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  if constexpr (METHOD == 0) integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a, sp);
+  else integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a, sp);
 }
 
 // ---------------------------------------------------------------------------------
@@ -549,6 +578,7 @@ struct IntegrateArgs {
   double* ssres;        // [W] or null
   int32_t* status;      // [W] or null
   int32_t half;         // 1: 32 walkers per wavefront (lanes 32-63 idle), 0: 64
+  int32_t split;        // 1: two waves integrate the same 64 walkers, each stores half the states
 };
 
 // parameter registers: the model's own P plus up to 4 '<state>0' initial-condition
@@ -562,11 +592,19 @@ __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const In
   constexpr int PMAX = kPmax<M>;
   int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool idle = false;
+  int sp = -1;
   if (ia.half) {  // walker = (wave, lane < 32); the upper half-wave idles (DOPRI5: dead lanes)
     const int lane = threadIdx.x & 63;
     gw = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32 + (lane & 31);
     idle = lane >= 32;
     if (METHOD == 0 && idle) return;
+  } else if (ia.split) {
+    // waves 2g and 2g+1 of a block run walker group g (64 walkers) redundantly; the even
+    // wave stores states [0, S/2), the odd one [S/2, S): twice the storing waves at the
+    // same store-instruction count, compute duplicated (it is hidden under the stores)
+    const int wv = threadIdx.x >> 6;
+    gw = ((int64_t)blockIdx.x * (blockDim.x >> 7) + (wv >> 1)) * 64 + (threadIdx.x & 63);
+    sp = __builtin_amdgcn_readfirstlane(wv & 1);
   }
   const bool active = gw < ia.W && !idle;
   const int64_t w = gw < ia.W ? gw : ia.W - 1;  // tail lanes shadow the last walker, never store
@@ -577,8 +615,8 @@ __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const In
 #pragma unroll
   for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
   Acc a = acc_init();
-  integrate_walker<M, PMAX, METHOD, TRAJ, NT>(pb, y, p, ia.traj, W, w, active, a);
-  if (active) {
+  integrate_walker<M, PMAX, METHOD, TRAJ, NT>(pb, y, p, ia.traj, W, w, active, a, sp);
+  if (active && sp <= 0) {
     if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
     if (ia.ssres) ia.ssres[w] = a.ssres;
     if (ia.status) ia.status[w] = finish(a);

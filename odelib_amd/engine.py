@@ -148,12 +148,14 @@ class Engine:
 
     # -- batched integrate -------------------------------------------------------------------
     def integrate(self, y0, theta, trajectory: bool = True, traj_out=None, nt_stores: bool = True,
-                  sync: bool = True, pipelined: bool = False, half_waves: bool = False):
+                  sync: bool = True, pipelined: bool = False, half_waves: bool = False,
+                  split_waves: bool = False):
         """y0 [S][W], theta [P][W] → dict(traj [T][S][W] | None, chi [W], ssres [W], status [W]).
 
         ``pipelined=True`` selects the opt-in producer/consumer RK4 trajectory kernel
         (same results; not faster on MI355X).  ``half_waves=True`` runs
-        32 walkers per wavefront (twice the waves; same results)."""
+        32 walkers per wavefront (twice the waves; same results).  ``split_waves=True``
+        runs two wavefronts per 64 walkers, each storing half of the states (same results)."""
         torch = self.torch
         pb = self.problem
         theta_t = theta if isinstance(theta, torch.Tensor) else np.asarray(theta)
@@ -171,7 +173,7 @@ class Engine:
         status = torch.empty(W, dtype=torch.int32, device=self.dev)
         self._sync_stream()
         flags = N.OE_ASYNC | (N.OE_NT_STORES if nt_stores else 0) | (N.OE_PIPE if pipelined else 0) \
-            | (N.OE_HALF_WAVES if half_waves else 0)
+            | (N.OE_HALF_WAVES if half_waves else 0) | (N.OE_SPLIT_WAVES if split_waves else 0)
         self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)
         if sync:
             torch.cuda.synchronize(self.dev)

@@ -97,6 +97,23 @@ def test_rk4_half_waves_match_full_waves(spec, W):
         assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
 
 
+@pytest.mark.parametrize("method", ["rk4", "dopri5"])
+@pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain5", "chain20"])
+@pytest.mark.parametrize("W", [1, 100, 4099])
+def test_split_waves_match_full_waves(method, spec, W):
+    """Two wavefronts per 64 walkers, each storing half of the states (OE_SPLIT_WAVES),
+    give the bits of the one-wave layout (trajectory, chi, R² residual, status),
+    incl. ragged tails and odd S."""
+    m = _model(spec, method)
+    theta = _walkers(spec, W)
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    eng = m.engine()
+    a = eng.integrate(y0, theta, split_waves=True)
+    b = eng.integrate(y0, theta, half_waves=False)
+    for key in ("traj", "chi", "ssres", "status"):
+        assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
+
+
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain8"])
 def test_rk4_substeps_bitwise(spec):
     m = _model(spec, "rk4", substeps=3)
