@@ -67,6 +67,10 @@ def pmc_traffic(args):
     import tempfile
     if shutil.which("rocprofv3") is None:
         return None, "rocprofv3 not found"
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        # already running under rocprofv3, whose library has initialised the GPU in this
+        # process: a child launched from here would be an exec after GPU initialisation
+        return None, "skipped (running under rocprofv3)"
     try:
         from tools.profile import pmc_pass
         out = tempfile.mkdtemp(prefix="bench_pmc_", dir=os.path.join(ROOT, "gpurun_out")

@@ -85,7 +85,8 @@ def main():
     # 1. kernel trace + stats (same command line as the bench run, minus the CPU leg)
     d = os.path.join(out, "trace")
     stdout = run(rocprof() + ["--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run", "--",
-                  sys.executable, "bench.py", "--no-cpu-baseline", "--no-extra-configs", *bench_args], args.timeout)
+                  sys.executable, "bench.py", "--no-cpu-baseline", "--no-extra-configs", "--no-pmc", *bench_args],
+                 args.timeout)
     bench_line = [l for l in stdout.splitlines() if l.startswith("{")]
     stats_csv = find(os.path.join(d, "**", "*kernel_stats.csv"))
     stats = read_csv(stats_csv)
