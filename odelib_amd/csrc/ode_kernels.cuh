@@ -132,6 +132,15 @@ __device__ __forceinline__ void st_row(__amdgpu_buffer_rsrc_t rsrc, uint32_t lan
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rsrc, lane_off, s_off, NT ? 2 : 0);
 }
 
+// Out-of-line transcendentals.  Inlined, ocml's f64 log/exp polynomial constants are
+// loop-invariant and get hoisted out of the time and MH loops into registers that stay
+// live for the whole kernel (~40 doubles in the MH kernel); behind a call they are
+// materialised per call (a call per observation / proposal, not per step).  A callee
+// starts with s_waitcnt vmcnt(0), which drains the trajectory stores in flight, so the
+// RK4 trajectory kernel (67 VGPRs either way) keeps the inline log (observe<S, true>).
+__device__ __attribute__((noinline)) double oe_log(double x) { return log(x); }
+__device__ __attribute__((noinline)) double oe_exp(double x) { return exp(x); }
+
 // NaN-propagating finiteness accumulator: a.nf becomes NaN iff some y[s] is NaN/inf.
 template <int S>
 __device__ __forceinline__ void check_finite(const double (&y)[S], Acc& a) {
@@ -172,7 +181,7 @@ __device__ __forceinline__ void store_row(int i, const double (&y)[S], double* _
 // Fold every observation recorded at grid index i into the likelihood (caller knows
 // one exists or checks `k`).  Finiteness is checked here and at the final state
 // (NaN/inf propagate through the RHS), not at every step.
-template <int S>
+template <int S, bool INLINE_LOG = false>
 __device__ __forceinline__ void observe(const DevProblem& pb, int i, const double (&y)[S], int& k, Acc& a) {
   const cptr<Obs> obs = kconst(pb.obs);
   if (!(k < pb.n_obs && obs[k].tidx == i)) return;
@@ -185,7 +194,7 @@ __device__ __forceinline__ void observe(const DevProblem& pb, int i, const doubl
     for (int s = 0; s < S; ++s)
       if ((mask >> s) & 1ull) c = c + y[s];  // increasing state order, as numpy's sum
     // chi term, in the operation order of stats.py:41
-    const double d = O - log(c);
+    const double d = O - (INLINE_LOG ? log(c) : oe_log(c));
     const double term = (d * d) / two_s2;
     if (__builtin_isfinite(term)) { a.chi += term; a.nvalid += 1; }
     // R² residual (stats.py:52 np.nansum skips NaN only)
@@ -207,12 +216,12 @@ __device__ __forceinline__ void observe_next(const DevProblem& pb, int i, const 
 }
 
 // Emit grid point i: row store + minimum + observations.
-template <int S, bool TRAJ, bool NT>
+template <int S, bool TRAJ, bool NT, bool INLINE_LOG = false>
 __device__ __forceinline__ void emit(const DevProblem& pb, int i, const double (&y)[S],
                                      double* __restrict__ traj, int64_t W, uint32_t off,
                                      bool active, int& k, Acc& a, int sp) {
   store_row<S, TRAJ, NT>(i, y, traj, W, off, active, a, sp);
-  observe<S>(pb, i, y, k, a);
+  observe<S, INLINE_LOG>(pb, i, y, k, a);
 }
 
 template <int S, bool TRAJ>
@@ -253,7 +262,7 @@ __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[
                                               const double (&p)[PMAX], double* traj,
                                               int64_t W, uint32_t off, bool active, Acc& a, int sp) {
   int k = 0;
-  emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a, sp);
+  emit<M::S, TRAJ, NT, TRAJ>(pb, 0, y, traj, W, off, active, k, a, sp);
   const int n = pb.substeps;
   const cptr<double> tab = kconst(pb.rk4);
   const cptr<Obs> obs = kconst(pb.obs);
@@ -279,7 +288,7 @@ __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[
     }
     if (i < pb.T) {  // i == next: an observed grid point
       interval(i);
-      emit<M::S, TRAJ, NT>(pb, i, y, traj, W, off, active, k, a, sp);
+      emit<M::S, TRAJ, NT, TRAJ>(pb, i, y, traj, W, off, active, k, a, sp);
       ++i;
     }
   }
@@ -391,6 +400,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
   int i = 1;
   double t_i = times[1];
   int nxt = (k < pb.n_obs) ? kconst(pb.obs)[k].tidx : 0x7fffffff;  // next observed index
+  double t_obs = (nxt < pb.T) ? times[nxt] : __builtin_inf();        // and its time
   int nst = 0;  // steps since the last grid point
   bool last_rej = false;
   while (i < pb.T) {
@@ -449,13 +459,14 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
       // point nearly always falls in the step, and k2..k6 die before the output loop).
       // Otherwise (observed points only): small S forms them on the first observed point
       // of the step, large S per observed point (lazily kept k's would spill).
-      constexpr bool kEager = TRAJ;
+      // S <= 8 without trajectory: formed once, eagerly, in the steps that reach the next
+      // observed time (the k's then die before the output loop); S > 8 per observed point.
+      const bool kEager = TRAJ || (!kLean && t_obs <= tn);
       constexpr bool kHoist = TRAJ || S <= 8;
-      bool have_dense = false;
       const double rh = 1.0 / h;  // one division per step, not per grid point
       double ydf[kHoist ? S : 1], bsp[kHoist ? S : 1], r4[kHoist ? S : 1], r5[kHoist ? S : 1];
       const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
-      if constexpr (kEager) {
+      if (kHoist && kEager) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           ydf[s] = yn[s] - y[s];
@@ -463,7 +474,6 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
           r4[s] = fma(-h, k7[s], ydf[s]) - bsp[s];
           r5[s] = fma(hd7, k7[s], fma(hd6, k6[s], fma(hd5, k5[s], fma(hd4, k4[s], fma(hd3, k3[s], hd1 * k1[s])))));
         }
-        have_dense = true;
       }
       while (i < pb.T && (kLean ? times[i] : t_i) <= tn) {
         const double ti = kLean ? times[i] : t_i;
@@ -476,17 +486,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
           } else {
             const double th = (ti - t) * rh;
             const double th1 = 1.0 - th;
-            if constexpr (kHoist) {
-              if (!kEager && !have_dense) {
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                  ydf[s] = yn[s] - y[s];
-                  bsp[s] = fma(h, k1[s], -ydf[s]);
-                  r4[s] = fma(-h, k7[s], ydf[s]) - bsp[s];
-                  r5[s] = fma(hd7, k7[s], fma(hd6, k6[s], fma(hd5, k5[s], fma(hd4, k4[s], fma(hd3, k3[s], hd1 * k1[s])))));
-                }
-                have_dense = true;
-              }
+            if constexpr (kHoist) {  // coefficients formed above (every emitted point has them)
 #pragma unroll
               for (int s = 0; s < S; ++s)
                 yo[s] = fma(th, fma(th1, fma(th, fma(th1, r5[s], r4[s]), bsp[s]), ydf[s]), y[s]);
@@ -510,7 +510,10 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
           } else {
             // (an evicted lane's state is NaN, so its dense output is NaN already)
             store_row<S, TRAJ, NT>(i, yo, traj, W, off, active, a, sp);
-            observe_next<S>(pb, i, yo, k, nxt, a);
+            if (i == nxt) {
+              observe_next<S>(pb, i, yo, k, nxt, a);
+              t_obs = (nxt < pb.T) ? times[nxt] : __builtin_inf();
+            }
           }
         }
         ++i;
@@ -699,7 +702,7 @@ __global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevP
         int r = r0;
         if (r == 0) {  // row 0 is the initial state
           put(half, 0, y);
-          observe<S>(pb, 0, y, k, a);
+          observe<S, true>(pb, 0, y, k, a);
           ++r;
         }
         while (r < r1) {
@@ -712,7 +715,7 @@ __global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevP
           if (r < r1) {  // observed row
             interval(r);
             put(half, r - r0, y);
-            observe<S>(pb, r, y, k, a);
+            observe<S, true>(pb, r, y, k, a);
             ++r;
           }
         }
@@ -838,6 +841,23 @@ struct MHArgs {
   int32_t* status;         // [W]
 };
 
+// Element w of a walker-minor row [W] through a buffer resource: row base and size in
+// SGPRs, the lane's byte offset w*8 in one VGPR.  With plain pointers the compiler
+// forms one 64-bit per-lane address per row, and since every row base is invariant in
+// the MH iteration loop it hoists them: two VGPRs per row, dozens of rows — the
+// register cost of a second wave per SIMD.
+struct Row {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ Row(const double* row, int64_t W)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)row, 0, (int)(W * 8), 0x00020000)) {}
+  __device__ __forceinline__ double ld(uint32_t off) const {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  }
+  __device__ __forceinline__ void st(uint32_t off, double v) const {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+  }
+};
+
 template <class M, int METHOD>
 __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma) {
   constexpr int S = M::S;
@@ -847,98 +867,102 @@ __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma
   const int64_t w = active ? gw : ma.W - 1;
   const int64_t W = ma.W;
   const int P = pb.P;
-  double th[PMAX], y0[S];
-#pragma unroll
-  for (int j = 0; j < PMAX; ++j) th[j] = (j < P) ? ma.theta[(int64_t)j * W + w] : 0.0;
-#pragma unroll
-  for (int s = 0; s < S; ++s) y0[s] = ma.y0[(int64_t)s * W + w];
+  // The chain state θ [P][W] and y0 [S][W] stays in HBM between iterations (a few loads
+  // per iteration against ~1000 integration steps): only the proposal is held in
+  // registers while integrating, which keeps the DOPRI5 MH kernel within the register
+  // budget of two waves per SIMD.  Tail lanes (w clamped to W-1) never store.
+  double* __restrict__ theta = ma.theta;
+  double* __restrict__ y0g = ma.y0;
+  const uint32_t off = (uint32_t)w * 8u;  // W <= 2^29 (oe_mh_run)
 
   if (ma.init) {  // a-priori fit (Samplers.py:88-91)
-    double y[S];
+    double th[PMAX], y[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) y[s] = y0[s];
+    for (int j = 0; j < PMAX; ++j) th[j] = (j < P) ? Row(theta + (int64_t)j * W, W).ld(off) : 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) y[s] = Row(y0g + (int64_t)s * W, W).ld(off);
     Acc a = acc_init();
     integrate_walker<M, PMAX, METHOD, false, false>(pb, y, th, nullptr, W, w, active, a);
     if (active) {
       const double chi = a.nvalid ? a.chi : __builtin_nan("");
-      ma.cur[w] = chi;
-      ma.cur[W + w] = 1.0 - a.ssres / pb.sstot;
-      ma.cur[2 * W + w] = -2.0 * (-chi) + 2.0 * (double)pb.pnum;
-      ma.cur[3 * W + w] = 0.0;
+      Row(ma.cur, W).st(off, chi);
+      Row(ma.cur + W, W).st(off, 1.0 - a.ssres / pb.sstot);
+      Row(ma.cur + 2 * W, W).st(off, -2.0 * (-chi) + 2.0 * (double)pb.pnum);
+      Row(ma.cur + 3 * W, W).st(off, 0.0);
       if (ma.status) ma.status[w] = finish(a);
     }
     return;
   }
 
-  double chi = ma.cur[w], rsq = ma.cur[W + w], aic = ma.cur[2 * W + w];
-  double nacc = ma.cur[3 * W + w];
+  double chi = Row(ma.cur, W).ld(off), rsq = Row(ma.cur + W, W).ld(off), aic = Row(ma.cur + 2 * W, W).ld(off);
+  double nacc = Row(ma.cur + 3 * W, W).ld(off);
   int32_t status = ma.status ? ma.status[w] : 0;
   const int PS = P + 5;
 
   for (int it = ma.it0; it < ma.it1; ++it) {
     // ---- proposal: θ' = exp(log θ + N(0, sd)) for walking parameters (Framework.py:107-122)
     double tn[PMAX];
-    const double* dz = ma.dz + (int64_t)(it - ma.draw_it0) * P * W + w;
+    const double* dz = ma.dz + (int64_t)(it - ma.draw_it0) * P * W;
 #pragma unroll
-    for (int j = 0; j < PMAX; ++j)
-      tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? exp(log(th[j]) + dz[(int64_t)j * W]) : th[j];
-    const double u = ma.u[(int64_t)(it - ma.draw_it0) * W + w];
+    for (int j = 0; j < PMAX; ++j) {
+      const double thj = (j < P) ? Row(theta + (int64_t)j * W, W).ld(off) : 0.0;
+      tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? oe_exp(oe_log(thj) + Row(dz + (int64_t)j * W, W).ld(off)) : thj;
+    }
+    const double u = Row(ma.u + (int64_t)(it - ma.draw_it0) * W, W).ld(off);
     // '<state>0' parameters drive initial states (Samplers.py:110-114)
-    double y[S], yp0[S];
+    double y[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int pi = ma.init_param[s];
-      yp0[s] = (ma.any_walk && pi >= 0) ? pick(tn, pi) : y0[s];
-      y[s] = yp0[s];
+      y[s] = (ma.any_walk && pi >= 0) ? pick(tn, pi) : Row(y0g + (int64_t)s * W, W).ld(off);
     }
     // ---- integrate + fused chi (Samplers.py:115-116)
     Acc a = acc_init();
     integrate_walker<M, PMAX, METHOD, false, false>(pb, y, tn, nullptr, W, w, active, a);
     const double chin = a.nvalid ? a.chi : __builtin_nan("");
     // ---- acceptance, in the reference's arithmetic (Samplers.py:124-127)
-    const double lr = exp(chi - chin);
-    const double accp = exp(log(lr));
-    if (accp > u) {
+    const double lr = oe_exp(chi - chin);
+    const double accp = oe_exp(oe_log(lr));
+    const bool acc = accp > u;
+    if (acc) {
       chi = chin;
       rsq = 1.0 - a.ssres / pb.sstot;
       aic = -2.0 * (-chi) + 2.0 * (double)pb.pnum;
-#pragma unroll
-      for (int j = 0; j < PMAX; ++j) th[j] = tn[j];
-#pragma unroll
-      for (int s = 0; s < S; ++s) y0[s] = yp0[s];
       nacc += 1.0;
       status = finish(a);
-    } else {
-      // reject: parameters restored, linked initial states follow them (Samplers.py:137-143)
+      if (active) {
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j)
+          if (j < P) Row(theta + (int64_t)j * W, W).st(off, tn[j]);
+      }
+    }
+    // linked initial states follow the current parameters: the accepted proposal, or
+    // on reject the restored ones (Samplers.py:110-114, :137-143)
+    if (ma.any_walk && active) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int pi = ma.init_param[s];
-        if (ma.any_walk && pi >= 0) y0[s] = pick(th, pi);
+        if (pi >= 0) Row(y0g + (int64_t)s * W, W).st(off, acc ? pick(tn, pi) : Row(theta + (int64_t)pi * W, W).ld(off));
       }
     }
     // ---- keep the sample after burn-in (Samplers.py:147-153)
     if (it > ma.burnin && active) {
-      double* row = ma.samples + (int64_t)(it - ma.row0) * PS * W + w;
+      double* row = ma.samples + (int64_t)(it - ma.row0) * PS * W;
 #pragma unroll
       for (int j = 0; j < PMAX; ++j)
-        if (j < P) row[(int64_t)j * W] = th[j];
-      row[(int64_t)P * W] = chi;
-      row[(int64_t)(P + 1) * W] = rsq;
-      row[(int64_t)(P + 2) * W] = aic;
-      row[(int64_t)(P + 3) * W] = (double)it;
-      row[(int64_t)(P + 4) * W] = nacc / (double)it;
+        if (j < P) Row(row + (int64_t)j * W, W).st(off, acc ? tn[j] : Row(theta + (int64_t)j * W, W).ld(off));
+      Row(row + (int64_t)P * W, W).st(off, chi);
+      Row(row + (int64_t)(P + 1) * W, W).st(off, rsq);
+      Row(row + (int64_t)(P + 2) * W, W).st(off, aic);
+      Row(row + (int64_t)(P + 3) * W, W).st(off, (double)it);
+      Row(row + (int64_t)(P + 4) * W, W).st(off, nacc / (double)it);
     }
   }
   if (active) {
-#pragma unroll
-    for (int j = 0; j < PMAX; ++j)
-      if (j < P) ma.theta[(int64_t)j * W + w] = th[j];
-#pragma unroll
-    for (int s = 0; s < S; ++s) ma.y0[(int64_t)s * W + w] = y0[s];
-    ma.cur[w] = chi;
-    ma.cur[W + w] = rsq;
-    ma.cur[2 * W + w] = aic;
-    ma.cur[3 * W + w] = nacc;
+    Row(ma.cur, W).st(off, chi);
+    Row(ma.cur + W, W).st(off, rsq);
+    Row(ma.cur + 2 * W, W).st(off, aic);
+    Row(ma.cur + 3 * W, W).st(off, nacc);
     if (ma.status) ma.status[w] = status;
   }
 }

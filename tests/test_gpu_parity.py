@@ -123,9 +123,14 @@ def test_rk4_substeps_bitwise(spec):
     assert np.array_equal(out["traj"], ref["traj"])
 
 
-@pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain6", "chain20"])
+@pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain6", "chain10", "chain20", "chain24", "chain32"])
 @pytest.mark.parametrize("W", [64, 200])
 def test_dopri5_vs_c_restatement(spec, W):
+    """Bitwise DOPRI5 vs the C restatement (chain10..chain32: the S > 8 register-limit
+    code path), and the chi of a no-trajectory launch (lazy dense output at observed
+    points only) equals the trajectory one.  The NEGATIVE status bit is "negative at an
+    output time", and a no-trajectory launch outputs observed times only, so only the
+    NONFINITE and MAXSTEP bits must agree between the two launches."""
     m = _model(spec, "dopri5")
     theta = _walkers(spec, W)
     y0, out = _run(m, theta)
@@ -133,6 +138,10 @@ def test_dopri5_vs_c_restatement(spec, W):
     assert np.array_equal(out["traj"], ref["traj"])
     np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
     assert np.array_equal(out["status"], ref["status"])
+    _, lean = _run(m, theta, y0=y0, trajectory=False)
+    for key in ("chi", "ssres"):
+        assert np.array_equal(lean[key], out[key], equal_nan=True), key
+    assert np.array_equal(lean["status"] & 5, out["status"] & 5)
 
 
 # --------------------------------------------------------------------- reference algorithm
