@@ -582,7 +582,18 @@ struct IntegrateArgs {
   int32_t* status;      // [W] or null
   int32_t half;         // 1: 32 walkers per wavefront (lanes 32-63 idle), 0: 64
   int32_t split;        // 1: two waves integrate the same 64 walkers, each stores half the states
+  int32_t xcd_remap;    // 1: the blocks dispatched to XCD x (blockIdx % 8, round-robin) take the
+                        //    x-th contiguous range of walker blocks (xcd_block)
 };
+
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2).  Map
+// them so XCD x owns one contiguous range of walker blocks: each XCD's trajectory stores
+// then form long runs within every row instead of 2 KB pieces interleaved with the other
+// seven XCDs (measured 3-10 % faster).  A bijection on [0, G) for any G.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t G) {
+  const int64_t q = G >> 3, r = G & 7, x = b & 7, j = b >> 3;
+  return x * q + (x < r ? x : r) + j;
+}
 
 // parameter registers: the model's own P plus up to 4 '<state>0' initial-condition
 // parameters (oe_problem_set enforces n_params <= kPmax<M>)
@@ -593,12 +604,13 @@ template <class M, int METHOD, bool TRAJ, bool NT>
 __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const IntegrateArgs ia) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
-  int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  int64_t gw = blk * blockDim.x + threadIdx.x;
   bool idle = false;
   int sp = -1;
   if (ia.half) {  // walker = (wave, lane < 32); the upper half-wave idles (DOPRI5: dead lanes)
     const int lane = threadIdx.x & 63;
-    gw = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32 + (lane & 31);
+    gw = (blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32 + (lane & 31);
     idle = lane >= 32;
     if (METHOD == 0 && idle) return;
   } else if (ia.split) {
@@ -606,7 +618,7 @@ __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const In
     // wave stores states [0, S/2), the odd one [S/2, S): twice the storing waves at the
     // same store-instruction count, compute duplicated (it is hidden under the stores)
     const int wv = threadIdx.x >> 6;
-    gw = ((int64_t)blockIdx.x * (blockDim.x >> 7) + (wv >> 1)) * 64 + (threadIdx.x & 63);
+    gw = (blk * (blockDim.x >> 7) + (wv >> 1)) * 64 + (threadIdx.x & 63);
     sp = __builtin_amdgcn_readfirstlane(wv & 1);
   }
   const bool active = gw < ia.W && !idle;

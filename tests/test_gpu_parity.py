@@ -99,7 +99,7 @@ def test_rk4_half_waves_match_full_waves(spec, W):
 
 @pytest.mark.parametrize("method", ["rk4", "dopri5"])
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain5", "chain20"])
-@pytest.mark.parametrize("W", [1, 100, 4099])
+@pytest.mark.parametrize("W", [1, 100, 4099, 8192])
 def test_split_waves_match_full_waves(method, spec, W):
     """Two wavefronts per 64 walkers, each storing half of the states (OE_SPLIT_WAVES),
     give the bits of the one-wave layout (trajectory, chi, R² residual, status),
@@ -110,8 +110,10 @@ def test_split_waves_match_full_waves(method, spec, W):
     eng = m.engine()
     a = eng.integrate(y0, theta, split_waves=True)
     b = eng.integrate(y0, theta, half_waves=False)
+    c = eng.integrate(y0, theta, xcd_remap=False)  # blockIdx-order walker blocks
     for key in ("traj", "chi", "ssres", "status"):
         assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
+        assert np.array_equal(c[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
 
 
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain8"])
