@@ -7,12 +7,17 @@ straight-line arithmetic over ``y[i]`` and ``ps[i]``; this module translates tha
 subset:
 
 * statements: assignments (also tuple unpacking ``a, b = ps[0], ps[1]`` / ``S, V = y``),
-  augmented assignments, docstrings, one final ``return`` of ``np.array([...])``,
-  a list or a tuple;
-* expressions: ``+ - * / **``, unary ``-``/``+``, numeric constants, ``y[k]``/``ps[k]``
-  with constant ``k``, ``t``, locals, numeric globals/closure constants, ``np.pi``/
-  ``math.pi``/``math.e``, ``a if c else b`` with comparisons, and the math calls in
-  ``_CALLS`` (numpy / math / builtins).
+  augmented assignments, docstrings, ``for i in range(...)`` loops with bounds known at
+  translation time (unrolled), local arrays (``dy = np.zeros(len(y))`` /
+  ``np.zeros_like(y)`` / ``np.empty(n)`` / ``[0.0] * n`` / a list literal) written and
+  read element-wise (``dy[i] = ...``, ``dy[i] += ...``), one final ``return`` of
+  ``np.array([...])``, a list, a tuple or a local array;
+* expressions: ``+ - * / **``, unary ``-``/``+``, numeric constants, ``y[k]``/``ps[k]``/
+  ``dy[k]`` with ``k`` an integer expression of constants, loop variables and ``len()``,
+  ``t``, locals, numeric globals/closure constants, ``np.pi``/``math.pi``/``math.e``,
+  ``a if c else b`` with comparisons, ``sum(...)`` / ``np.sum(...)`` of a slice or local
+  array (expanded in numpy's summation order), and the math calls in ``_CALLS``
+  (numpy / math / builtins).
 
 Python evaluates ``a*b*c`` as ``(a*b)*c`` in IEEE double; the emitted C keeps every
 parenthesisation and the library compiles with -ffp-contract=off, so each emitted
@@ -141,29 +146,101 @@ class _Translator:
         self.env = set()
         self.stmts = []     # (name, expr-IR)
         self.outs = None
+        self.ints = {}      # translation-time integers: loop variables, len(...), integer locals
+        self.arrays = {}    # local arrays: name -> [element variable name or None (unset)]
 
-    # ---- expressions -> IR ----
+    # ---- translation-time integers (indices, loop bounds) ----
+    def length_of(self, name):
+        if name == self.yname:
+            return self.S
+        if name == self.pname:
+            return self.P
+        if name in self.arrays:
+            return len(self.arrays[name])
+        raise Unsupported(f"len({name})")
+
+    def intexpr(self, n):
+        if isinstance(n, ast.Constant) and isinstance(n.value, int) and not isinstance(n.value, bool):
+            return n.value
+        if isinstance(n, ast.Name):
+            if n.id in self.ints:
+                return self.ints[n.id]
+            if n.id in self.consts and float(self.consts[n.id]).is_integer() and n.id not in self.env:
+                return int(self.consts[n.id])
+            raise Unsupported(f"{n.id!r} is not an integer known at translation time")
+        if isinstance(n, ast.Call) and isinstance(n.func, ast.Name) and n.func.id == "len" and len(n.args) == 1 \
+                and isinstance(n.args[0], ast.Name):
+            return self.length_of(n.args[0].id)
+        if isinstance(n, ast.Call) and isinstance(n.func, ast.Name) and n.func.id == "int" and len(n.args) == 1:
+            return self.intexpr(n.args[0])
+        if isinstance(n, ast.UnaryOp) and isinstance(n.op, ast.USub):
+            return -self.intexpr(n.operand)
+        if isinstance(n, ast.BinOp):
+            a, b = self.intexpr(n.left), self.intexpr(n.right)
+            ops = {ast.Add: lambda: a + b, ast.Sub: lambda: a - b, ast.Mult: lambda: a * b,
+                   ast.FloorDiv: lambda: a // b, ast.Mod: lambda: a % b}
+            if type(n.op) in ops:
+                return ops[type(n.op)]()
+        raise Unsupported("integer expression")
+
+    def is_int(self, n):
+        """True for an integer expression known at translation time (no y/ps/t data)."""
+        if isinstance(n, ast.Constant) and isinstance(n.value, float):
+            return False
+        try:
+            self.intexpr(n)
+            return True
+        except Unsupported:
+            return False
+
     def index(self, node, length):
-        if isinstance(node, ast.Constant) and isinstance(node.value, int) and not isinstance(node.value, bool):
-            k = node.value
-        elif isinstance(node, ast.UnaryOp) and isinstance(node.op, ast.USub) and isinstance(node.operand, ast.Constant):
-            k = -node.operand.value
-        else:
-            raise Unsupported("only constant integer indices into y / ps are supported")
+        k = self.intexpr(node)
         if k < 0:
             k += length
         if not (0 <= k < length):
             raise Unsupported(f"index {k} out of range (length {length})")
         return k
 
+    def elements(self, n):
+        """IR of the elements of y, ps, a local array, or a slice of one (for sum)."""
+        if isinstance(n, ast.Name) and (n.id in (self.yname, self.pname) or n.id in self.arrays):
+            base, sl = n.id, None
+        elif isinstance(n, ast.Subscript) and isinstance(n.value, ast.Name) and isinstance(n.slice, ast.Slice):
+            base, sl = n.value.id, n.slice
+        else:
+            raise Unsupported("sum() needs y, ps, a local array or a slice of one")
+        length = self.length_of(base)
+        idx = list(range(length))
+        if sl is not None:
+            lo = self.intexpr(sl.lower) if sl.lower is not None else None
+            hi = self.intexpr(sl.upper) if sl.upper is not None else None
+            st = self.intexpr(sl.step) if sl.step is not None else None
+            idx = idx[slice(lo, hi, st)]
+        return [self.element(base, k) for k in idx]
+
+    def element(self, base, k):
+        if base == self.yname:
+            return ("y", k)
+        if base == self.pname:
+            return ("ps", k)
+        var = self.arrays[base][k]
+        if var is None:
+            raise Unsupported(f"{base}[{k}] read before it is set")
+        return ("var", var)
+
+    # ---- expressions -> IR ----
     def expr(self, n):
         if isinstance(n, ast.Constant):
             if isinstance(n.value, bool) or not isinstance(n.value, (int, float)):
                 raise Unsupported(f"constant {n.value!r}")
             return ("const", float(n.value))
         if isinstance(n, ast.Name):
+            if n.id in self.arrays:
+                raise Unsupported(f"array {n.id!r} used as a scalar")
             if n.id in self.env:
                 return ("var", n.id)
+            if n.id in self.ints:
+                return ("const", float(self.ints[n.id]))
             if n.id == self.tname:
                 return ("t",)
             if n.id in self.consts:
@@ -181,6 +258,8 @@ class _Translator:
                 return ("y", self.index(idx, self.S))
             if n.value.id == self.pname:
                 return ("ps", self.index(idx, self.P))
+            if n.value.id in self.arrays:
+                return self.element(n.value.id, self.index(idx, len(self.arrays[n.value.id])))
             raise Unsupported(f"subscript of {n.value.id!r}")
         if isinstance(n, ast.UnaryOp):
             if isinstance(n.op, ast.USub):
@@ -205,6 +284,13 @@ class _Translator:
             raise Unsupported("binary operator")
         if isinstance(n, ast.Call):
             f = n.func
+            is_sum = (isinstance(f, ast.Name) and f.id == "sum") or (
+                isinstance(f, ast.Attribute) and isinstance(f.value, ast.Name) and f.value.id in ("np", "numpy")
+                and f.attr == "sum")
+            if is_sum:
+                if len(n.args) != 1 or n.keywords:
+                    raise Unsupported("sum() of one sequence")
+                return self.summation(self.elements(n.args[0]), pairwise=not isinstance(f, ast.Name))
             if isinstance(f, ast.Attribute) and isinstance(f.value, ast.Name) and f.value.id in _MODULES:
                 name = f.attr
             elif isinstance(f, ast.Name) and f.id in ("abs", "max", "min", "pow"):
@@ -220,6 +306,31 @@ class _Translator:
         if isinstance(n, ast.IfExp):
             return ("ifexp", self.cond(n.test), self.expr(n.body), self.expr(n.orelse))
         raise Unsupported(type(n).__name__)
+
+    @staticmethod
+    def summation(xs, pairwise):
+        """Python's sum() adds left to right from 0; numpy's add.reduce (pairwise_sum)
+        does the same below 8 elements and otherwise runs 8 strided accumulators,
+        combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the remainder."""
+        if not xs:
+            return ("const", 0.0)
+        if not pairwise or len(xs) < 8:
+            acc = xs[0]  # 0 + x0 == x0
+            for x in xs[1:]:
+                acc = ("bin", "+", acc, x)
+            return acc
+        if len(xs) > 128:
+            raise Unsupported("np.sum of more than 128 elements")
+        r = list(xs[:8])
+        m = len(xs) - len(xs) % 8
+        for i in range(8, m, 8):
+            for j in range(8):
+                r[j] = ("bin", "+", r[j], xs[i + j])
+        acc = ("bin", "+", ("bin", "+", ("bin", "+", r[0], r[1]), ("bin", "+", r[2], r[3])),
+               ("bin", "+", ("bin", "+", r[4], r[5]), ("bin", "+", r[6], r[7])))
+        for x in xs[m:]:
+            acc = ("bin", "+", acc, x)
+        return acc
 
     def cond(self, n):
         if isinstance(n, ast.Compare) and len(n.ops) == 1 and type(n.ops[0]) in _CMP:
@@ -246,34 +357,125 @@ class _Translator:
         if body and isinstance(body[0], ast.Expr) and isinstance(body[0].value, ast.Constant) \
                 and isinstance(body[0].value.value, str):
             body = body[1:]
+        self.block(body)
+        if self.outs is None:
+            raise Unsupported("no return")
+        if len(self.outs) != self.S:
+            raise Unsupported(f"returns {len(self.outs)} derivatives for {self.S} states")
+
+    _AUG = {ast.Add: "+", ast.Sub: "-", ast.Mult: "*", ast.Div: "/"}
+
+    def block(self, body):
         for st in body:
             if self.outs is not None:
                 raise Unsupported("statements after return")
             if isinstance(st, ast.Assign) and len(st.targets) == 1:
                 tgt = st.targets[0]
                 if isinstance(tgt, ast.Name):
-                    self.assign([tgt.id], [self.expr(st.value)])
+                    arr = self.array_value(st.value)
+                    if arr is not None:
+                        self.new_array(tgt.id, arr)
+                    elif tgt.id in self.arrays:
+                        raise Unsupported(f"array {tgt.id!r} reassigned")
+                    elif tgt.id not in self.env and self.is_int(st.value):
+                        self.ints[tgt.id] = self.intexpr(st.value)  # e.g. n = len(y)
+                    else:
+                        self.ints.pop(tgt.id, None)
+                        self.assign([tgt.id], [self.expr(st.value)])
+                elif isinstance(tgt, ast.Subscript) and isinstance(tgt.value, ast.Name) and tgt.value.id in self.arrays:
+                    self.set_element(tgt, self.expr(st.value))
                 elif isinstance(tgt, (ast.Tuple, ast.List)) and all(isinstance(e, ast.Name) for e in tgt.elts):
                     names = [e.id for e in tgt.elts]
                     self.assign(names, self.seq(st.value, len(names)))
                 else:
                     raise Unsupported("assignment target")
-            elif isinstance(st, ast.AugAssign) and isinstance(st.target, ast.Name) and st.target.id in self.env:
-                op = {ast.Add: "+", ast.Sub: "-", ast.Mult: "*", ast.Div: "/"}.get(type(st.op))
-                if op is None:
-                    raise Unsupported("augmented operator")
-                self.assign([st.target.id], [("bin", op, ("var", st.target.id), self.expr(st.value))])
+            elif isinstance(st, ast.AugAssign) and type(st.op) in self._AUG:
+                op = self._AUG[type(st.op)]
+                if isinstance(st.target, ast.Name) and st.target.id in self.ints and self.is_int(st.value) \
+                        and op in "+-*":
+                    a, b = self.ints[st.target.id], self.intexpr(st.value)
+                    self.ints[st.target.id] = a + b if op == "+" else a - b if op == "-" else a * b
+                elif isinstance(st.target, ast.Name) and st.target.id in self.ints:
+                    old = ("const", float(self.ints.pop(st.target.id)))
+                    self.assign([st.target.id], [("bin", op, old, self.expr(st.value))])
+                elif isinstance(st.target, ast.Name) and st.target.id in self.env and st.target.id not in self.arrays:
+                    self.assign([st.target.id], [("bin", op, ("var", st.target.id), self.expr(st.value))])
+                elif isinstance(st.target, ast.Subscript) and isinstance(st.target.value, ast.Name) \
+                        and st.target.value.id in self.arrays:
+                    old = self.expr(st.target)
+                    self.set_element(st.target, ("bin", op, old, self.expr(st.value)))
+                else:
+                    raise Unsupported("augmented assignment target")
+            elif isinstance(st, ast.For):
+                self.unroll(st)
             elif isinstance(st, ast.Return):
                 self.outs = self.returned(st.value)
             elif isinstance(st, ast.Pass):
                 continue
             else:
                 raise Unsupported(type(st).__name__)
-        if self.outs is None:
-            raise Unsupported("no return")
-        if len(self.outs) != self.S:
-            raise Unsupported(f"returns {len(self.outs)} derivatives for {self.S} states")
 
+    def unroll(self, st):
+        it = st.iter
+        if not (isinstance(st.target, ast.Name) and isinstance(it, ast.Call) and isinstance(it.func, ast.Name)
+                and it.func.id == "range" and 1 <= len(it.args) <= 3 and not it.keywords and not st.orelse):
+            raise Unsupported("only `for i in range(...)` loops with known bounds")
+        bounds = [self.intexpr(a) for a in it.args]
+        values = range(*bounds)
+        if len(values) > 4096:
+            raise Unsupported("loop longer than 4096 iterations")
+        name = st.target.id
+        if name in self.env or name in self.arrays:
+            raise Unsupported(f"loop variable {name!r} shadows a local")
+        for v in values:
+            self.ints[name] = v
+            self.block(st.body)
+            if self.outs is not None:
+                raise Unsupported("return inside a loop")
+
+    def array_value(self, v):
+        """Element IR list if `v` constructs a local array, else None."""
+        def length(arg):
+            return self.length_of(arg.id) if isinstance(arg, ast.Name) and (
+                arg.id in (self.yname, self.pname) or arg.id in self.arrays) else None
+        if isinstance(v, ast.Call) and isinstance(v.func, ast.Attribute) and isinstance(v.func.value, ast.Name) \
+                and v.func.value.id in ("np", "numpy") and len(v.args) == 1:
+            attr, arg = v.func.attr, v.args[0]
+            if attr in ("zeros", "empty"):
+                n = self.intexpr(arg)
+                return [("const", 0.0) if attr == "zeros" else None] * n
+            if attr in ("zeros_like", "empty_like"):
+                n = length(arg)
+                if n is None:
+                    raise Unsupported(f"np.{attr} of a non-array")
+                return [("const", 0.0) if attr == "zeros_like" else None] * n
+            if attr in ("array", "asarray") and isinstance(arg, (ast.List, ast.Tuple)):
+                return [self.expr(e) for e in arg.elts]
+            return None
+        if isinstance(v, ast.BinOp) and isinstance(v.op, ast.Mult) and isinstance(v.left, ast.List) \
+                and len(v.left.elts) == 1:
+            return [self.expr(v.left.elts[0])] * self.intexpr(v.right)
+        if isinstance(v, ast.List):
+            return [self.expr(e) for e in v.elts]
+        return None
+
+    def new_array(self, name, elems):
+        if name in self.env or name in (self.yname, self.pname, self.tname):
+            raise Unsupported(f"array {name!r} shadows a scalar or an argument")
+        self.arrays[name] = [None] * len(elems)
+        for k, e in enumerate(elems):
+            if e is not None:
+                self.arrays[name][k] = self.bind(f"{name}__{k}", e)
+
+    def set_element(self, tgt, e):
+        name = tgt.value.id
+        k = self.index(tgt.slice, len(self.arrays[name]))
+        self.arrays[name][k] = self.bind(f"{name}__{k}", e)
+
+    def bind(self, var, e):
+        self.stmts.append((var, e))
+        self.env.add(var)
+        return var
     def assign(self, names, exprs):
         if len(names) == 1:
             self.stmts.append((names[0], exprs[0]))
@@ -295,7 +497,9 @@ class _Translator:
             v = v.args[0]
         if isinstance(v, (ast.List, ast.Tuple)):
             return [self.expr(e) for e in v.elts]
-        raise Unsupported("return value must be np.array([...]), a list or a tuple")
+        if isinstance(v, ast.Name) and v.id in self.arrays:
+            return [self.element(v.id, k) for k in range(len(self.arrays[v.id]))]
+        raise Unsupported("return value must be np.array([...]), a list, a tuple or a local array")
 
 
 def _c(e) -> str:

@@ -94,14 +94,15 @@ def walker_thetas(name, W=8, seed=0):
     return np.array([[base[p] * np.exp(0.05 * z[w, j]) for j, p in enumerate(pn)] for w in range(W)])
 
 
-def chain_problem(n, method="rk4", substeps=1, T=1000, **kw):
-    """FitProblem of the synthetic N-state chain with the demo observations (H, V)."""
+def chain_problem(n, method="rk4", substeps=1, T=1000, ode=None, device_model="chain", **kw):
+    """FitProblem of the synthetic N-state chain with the demo observations (H, V);
+    ``ode`` replaces the callable (``device_model=None``: resolve it by probing)."""
     from odelib_amd import ModelFramework, parameter
     df = demo_df({"virus": "V", "host": "H"})
     snames = ["S"] + [f"I{k}" for k in range(1, n - 1)] + ["V"]
     th = THETA["two_i"]
-    m = ModelFramework(ODE=chain_rhs(n), parameter_names=list(th), state_names=snames, dataframe=df,
-                       state_summations={"H": snames[:-1]}, t_steps=T, S=5236900, method=method,
-                       rk4_substeps=substeps, device_model="chain",
+    m = ModelFramework(ODE=ode if ode is not None else chain_rhs(n), parameter_names=list(th), state_names=snames,
+                       dataframe=df, state_summations={"H": snames[:-1]}, t_steps=T, S=5236900, method=method,
+                       rk4_substeps=substeps, device_model=device_model,
                        **{p: parameter(init_value=v) for p, v in th.items()}, **kw)
     return m

@@ -59,6 +59,51 @@ def test_general_subset_translates():
     assert "?" in tr2.c_body and "pow(" in tr2.c_body
 
 
+def chain_loop(y, t, ps):
+    """The synthetic N-state chain as a user would write it: a loop
+    over the compartments into a preallocated array."""
+    mu, phi, beta, lam, tau = ps
+    n = len(y)
+    dy = np.zeros(n)
+    inf = phi * y[0] * y[-1]
+    dy[0] = mu * y[0] - inf
+    dy[1] = inf - tau * y[1]
+    for k in range(2, n - 2):
+        dy[k] = tau * y[k - 1] - tau * y[k]
+    dy[n - 2] = tau * y[n - 3] - lam * y[n - 2]
+    dy[-1] = beta * lam * y[n - 2] - inf
+    return dy
+
+
+def pooled(y, t, ps):
+    """Sums over slices (built-in sum and numpy's pairwise np.sum), augmented element
+    updates and a loop variable used as a number."""
+    d = np.zeros_like(y)
+    total = np.sum(y)
+    head = sum(y[: len(y) // 2])
+    for i in range(len(y)):
+        d[i] = ps[0] * total - ps[1] * y[i]
+        d[i] += head * (i + 1) * 1e-3
+    return d
+
+
+@pytest.mark.parametrize("n", [4, 7, 8, 12, 20, 33])
+def test_loops_arrays_and_sums_translate_exactly(n):
+    """Unrolled loops, local arrays and sums keep Python's operation order: the
+    translation evaluates bit-for-bit like the callable (np.sum in numpy's pairwise
+    order: sequential below 8 elements, 8 strided accumulators above)."""
+    tr = transpile(chain_loop, n, 5)
+    tp = transpile(pooled, n, 2)
+    rs = np.random.RandomState(n)
+    for _ in range(25):
+        y = rs.uniform(0, 1, n) * 10.0 ** rs.uniform(-3, 7, n)
+        ps = rs.uniform(0.1, 3, 5)
+        t = rs.uniform(0, 3)
+        assert np.array_equal(tr.evaluate(y, t, ps), chain_loop(y, t, ps))
+        assert np.array_equal(tp.evaluate(y, t, ps[:2]), pooled(y, t, ps[:2]))
+    assert "for" not in tr.c_body and f"dy[{n - 1}]" in tr.c_body
+
+
 def test_unsupported_constructs_are_rejected():
     def loop(y, t, ps):
         out = []
@@ -67,7 +112,7 @@ def test_unsupported_constructs_are_rejected():
         return out
 
     def dyn_index(y, t, ps):
-        i = 0
+        i = int(ps[0])
         return [y[i]]
 
     def wrong_len(y, t, ps):
