@@ -10,8 +10,11 @@ subset:
   augmented assignments, docstrings, ``for i in range(...)`` loops with bounds known at
   translation time (unrolled), local arrays (``dy = np.zeros(len(y))`` /
   ``np.zeros_like(y)`` / ``np.empty(n)`` / ``[0.0] * n`` / a list literal) written and
-  read element-wise (``dy[i] = ...``, ``dy[i] += ...``), one final ``return`` of
-  ``np.array([...])``, a list, a tuple or a local array;
+  read element-wise (``dy[i] = ...``, ``dy[i] += ...``) or by slice (``dy[2:-2] = ...``,
+  ``out[1:] += ...``, ``out *= ...``), one final ``return`` of ``np.array([...])``, a
+  list, a tuple, a local array or an array expression;
+* whole-array numpy arithmetic (``-k * y + np.exp(-y / 10.0) * t``, slices, broadcasting
+  of scalars) is expanded element by element in numpy's operation order;
 * expressions: ``+ - * / **``, unary ``-``/``+``, numeric constants, ``y[k]``/``ps[k]``/
   ``dy[k]`` with ``k`` an integer expression of constants, loop variables and ``len()``,
   ``t``, locals, numeric globals/closure constants, ``np.pi``/``math.pi``/``math.e``,
@@ -228,7 +231,67 @@ class _Translator:
             raise Unsupported(f"{base}[{k}] read before it is set")
         return ("var", var)
 
-    # ---- expressions -> IR ----
+    def listexpr(self, n):
+        """Scalar IR of a Python list built from literals, `+` concatenation and `*` repetition."""
+        if isinstance(n, (ast.List, ast.Tuple)):
+            return [self.expr(e) for e in n.elts]
+        if isinstance(n, ast.BinOp) and isinstance(n.op, ast.Add):
+            return self.listexpr(n.left) + self.listexpr(n.right)
+        if isinstance(n, ast.BinOp) and isinstance(n.op, ast.Mult):
+            if isinstance(n.left, (ast.List, ast.Tuple, ast.BinOp)) and self.is_int(n.right):
+                return self.listexpr(n.left) * self.intexpr(n.right)
+            if isinstance(n.right, (ast.List, ast.Tuple, ast.BinOp)) and self.is_int(n.left):
+                return self.listexpr(n.right) * self.intexpr(n.left)
+        raise Unsupported("list expression")
+
+    # ---- whole-array (numpy elementwise) expressions -> list of scalar IR ----
+    _BINOPS = {ast.Add: "+", ast.Sub: "-", ast.Mult: "*", ast.Div: "/"}
+
+    def vexpr(self, n):
+        """Elementwise IR of an array-valued expression (y, ps, a local array, a slice of
+        one, or numpy arithmetic / ufunc calls involving them); None if `n` is scalar."""
+        if isinstance(n, ast.Name):
+            if n.id in (self.yname, self.pname) or n.id in self.arrays:
+                return self.elements(n)
+            return None
+        if isinstance(n, ast.Subscript) and isinstance(n.slice, ast.Slice):
+            return self.elements(n)
+        if isinstance(n, ast.UnaryOp) and isinstance(n.op, (ast.USub, ast.UAdd)):
+            v = self.vexpr(n.operand)
+            if v is None or isinstance(n.op, ast.UAdd):
+                return v
+            return [("neg", e) for e in v]
+        if isinstance(n, ast.BinOp) and (type(n.op) in self._BINOPS or isinstance(n.op, ast.Pow)):
+            va, vb = self.vexpr(n.left), self.vexpr(n.right)
+            if va is None and vb is None:
+                return None
+            if va is not None and vb is not None and len(va) != len(vb):
+                raise Unsupported("array lengths differ")
+            m = len(va if va is not None else vb)
+            la = va if va is not None else [self.expr(n.left)] * m
+            lb = vb if vb is not None else [self.expr(n.right)] * m
+            if isinstance(n.op, ast.Pow):
+                return [("bin", "sq", a, a) if b == ("const", 2.0) else ("bin", "pow", a, b) for a, b in zip(la, lb)]
+            return [("bin", self._BINOPS[type(n.op)], a, b) for a, b in zip(la, lb)]
+        if isinstance(n, ast.Call) and isinstance(n.func, ast.Attribute) and isinstance(n.func.value, ast.Name) \
+                and n.func.value.id in ("np", "numpy"):
+            if n.func.attr in ("array", "asarray") and len(n.args) == 1 and not n.keywords:
+                a = n.args[0]
+                if isinstance(a, (ast.List, ast.Tuple)) or (isinstance(a, ast.BinOp) and self.vexpr(a) is None):
+                    return self.listexpr(a)
+                return self.vexpr(a)
+            if n.func.attr in _CALLS and not n.keywords:
+                vs = [self.vexpr(a) for a in n.args]
+                if all(v is None for v in vs):
+                    return None
+                m = {len(v) for v in vs if v is not None}
+                if len(m) != 1 or len(n.args) != _CALLS[n.func.attr][2]:
+                    raise Unsupported(f"np.{n.func.attr} arguments")
+                m = m.pop()
+                cols = [v if v is not None else [self.expr(a)] * m for v, a in zip(vs, n.args)]
+                return [("call", n.func.attr, list(args)) for args in zip(*cols)]
+        return None
+
     def expr(self, n):
         if isinstance(n, ast.Constant):
             if isinstance(n.value, bool) or not isinstance(n.value, (int, float)):
@@ -383,7 +446,10 @@ class _Translator:
                         self.ints.pop(tgt.id, None)
                         self.assign([tgt.id], [self.expr(st.value)])
                 elif isinstance(tgt, ast.Subscript) and isinstance(tgt.value, ast.Name) and tgt.value.id in self.arrays:
-                    self.set_element(tgt, self.expr(st.value))
+                    if isinstance(tgt.slice, ast.Slice):
+                        self.set_slice(tgt, lambda old, new: new, st.value)
+                    else:
+                        self.set_element(tgt, self.expr(st.value))
                 elif isinstance(tgt, (ast.Tuple, ast.List)) and all(isinstance(e, ast.Name) for e in tgt.elts):
                     names = [e.id for e in tgt.elts]
                     self.assign(names, self.seq(st.value, len(names)))
@@ -401,9 +467,16 @@ class _Translator:
                 elif isinstance(st.target, ast.Name) and st.target.id in self.env and st.target.id not in self.arrays:
                     self.assign([st.target.id], [("bin", op, ("var", st.target.id), self.expr(st.value))])
                 elif isinstance(st.target, ast.Subscript) and isinstance(st.target.value, ast.Name) \
+                        and st.target.value.id in self.arrays and isinstance(st.target.slice, ast.Slice):
+                    self.set_slice(st.target, lambda old, new, op=op: ("bin", op, old, new), st.value)
+                elif isinstance(st.target, ast.Subscript) and isinstance(st.target.value, ast.Name) \
                         and st.target.value.id in self.arrays:
                     old = self.expr(st.target)
                     self.set_element(st.target, ("bin", op, old, self.expr(st.value)))
+                elif isinstance(st.target, ast.Name) and st.target.id in self.arrays:
+                    whole = ast.Subscript(value=ast.Name(id=st.target.id, ctx=ast.Load()),
+                                          slice=ast.Slice(lower=None, upper=None, step=None), ctx=ast.Store())
+                    self.set_slice(whole, lambda old, new, op=op: ("bin", op, old, new), st.value)
                 else:
                     raise Unsupported("augmented assignment target")
             elif isinstance(st, ast.For):
@@ -449,15 +522,11 @@ class _Translator:
                 if n is None:
                     raise Unsupported(f"np.{attr} of a non-array")
                 return [("const", 0.0) if attr == "zeros_like" else None] * n
-            if attr in ("array", "asarray") and isinstance(arg, (ast.List, ast.Tuple)):
-                return [self.expr(e) for e in arg.elts]
-            return None
-        if isinstance(v, ast.BinOp) and isinstance(v.op, ast.Mult) and isinstance(v.left, ast.List) \
-                and len(v.left.elts) == 1:
-            return [self.expr(v.left.elts[0])] * self.intexpr(v.right)
-        if isinstance(v, ast.List):
-            return [self.expr(e) for e in v.elts]
-        return None
+            return self.vexpr(v)  # np.array(...) / np.asarray(...) / elementwise ufuncs
+        if isinstance(v, ast.List) or (isinstance(v, ast.BinOp) and (
+                isinstance(v.left, (ast.List, ast.Tuple)) or isinstance(v.right, (ast.List, ast.Tuple)))):
+            return self.listexpr(v)
+        return self.vexpr(v)
 
     def new_array(self, name, elems):
         if name in self.env or name in (self.yname, self.pname, self.tname):
@@ -466,6 +535,27 @@ class _Translator:
         for k, e in enumerate(elems):
             if e is not None:
                 self.arrays[name][k] = self.bind(f"{name}__{k}", e)
+
+    def set_slice(self, tgt, combine, value):
+        """arr[a:b:c] = value / arr[a:b:c] op= value, elementwise (value broadcast if scalar)."""
+        name = tgt.value.id
+        sl = tgt.slice
+        idx = list(range(len(self.arrays[name])))[slice(
+            self.intexpr(sl.lower) if sl.lower is not None else None,
+            self.intexpr(sl.upper) if sl.upper is not None else None,
+            self.intexpr(sl.step) if sl.step is not None else None)]
+        vec = self.vexpr(value)
+        if vec is None:
+            vec = [self.expr(value)] * len(idx)
+        if len(vec) != len(idx):
+            raise Unsupported("slice assignment length mismatch")
+        olds = [self.element(name, k) if self.arrays[name][k] is not None else None for k in idx]
+        news = [combine(o, v) if o is not None or combine(("const", 0.0), v) == v else None
+                for o, v in zip(olds, vec)]
+        if any(nv is None for nv in news):
+            raise Unsupported(f"{name}[...] updated before it is set")
+        for k, nv in zip(idx, news):  # all right-hand sides read before any element is written
+            self.arrays[name][k] = self.bind(f"{name}__{k}", nv)
 
     def set_element(self, tgt, e):
         name = tgt.value.id
@@ -497,9 +587,13 @@ class _Translator:
             v = v.args[0]
         if isinstance(v, (ast.List, ast.Tuple)):
             return [self.expr(e) for e in v.elts]
-        if isinstance(v, ast.Name) and v.id in self.arrays:
-            return [self.element(v.id, k) for k in range(len(self.arrays[v.id]))]
-        raise Unsupported("return value must be np.array([...]), a list, a tuple or a local array")
+        if isinstance(v, ast.BinOp) and (isinstance(v.left, (ast.List, ast.Tuple))
+                                         or isinstance(v.right, (ast.List, ast.Tuple))):
+            return self.listexpr(v)
+        vec = self.vexpr(v)
+        if vec is not None:
+            return vec
+        raise Unsupported("return value must be np.array([...]), a list, a tuple or an array expression")
 
 
 def _c(e) -> str:

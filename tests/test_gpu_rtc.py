@@ -5,7 +5,7 @@ import pytest
 
 from helpers import CONFIGS, THETA, demo_df, product_model, walker_thetas
 from oracle import cpu_ref
-from test_transpile import chain_loop, sat_infection
+from test_transpile import chain_loop, sat_infection, vec_chain
 
 pytestmark = pytest.mark.gpu
 
@@ -93,8 +93,9 @@ def test_transpiled_mh_matches_builtin_mh():
     np.testing.assert_allclose(rb["samples"].cpu().numpy(), ra["samples"].cpu().numpy(), rtol=1e-9)
 
 
+@pytest.mark.parametrize("ode", [chain_loop, vec_chain], ids=["loop", "slices"])
 @pytest.mark.parametrize("method", ["rk4", "dopri5"])
-def test_loop_written_chain_model_via_rtc(method):
+def test_loop_written_chain_model_via_rtc(method, ode):
     """The chain model written with a loop and a local array, forced onto the hipRTC
     path (device_model='rtc'): same trajectories as the compiled Chain<12> up to the
     fused vs separate multiply-subtract rounding, and within 1e-6 of tight odeint.
@@ -102,14 +103,14 @@ def test_loop_written_chain_model_via_rtc(method):
     from helpers import chain_problem
     n = 12
     a = chain_problem(n, method=method)
-    b = chain_problem(n, method=method, ode=chain_loop, device_model="rtc")
+    b = chain_problem(n, method=method, ode=ode, device_model="rtc")
     assert b.fit_problem().custom_source is not None
-    assert chain_problem(n, method=method, ode=chain_loop, device_model=None).fit_problem().custom_source is None
+    assert chain_problem(n, method=method, ode=ode, device_model=None).fit_problem().custom_source is None
     theta = walker_thetas("two_i", 96).T.copy()
     y0, ra = _run(a, theta)
     _, rb = _run(b, theta)
     np.testing.assert_allclose(rb["traj"], ra["traj"], rtol=1e-9, atol=1e-4)
     np.testing.assert_allclose(rb["chi"], ra["chi"], rtol=1e-9)
     for w in (0, 50, 95):
-        tight = cpu_ref.odeint_traj(chain_loop, y0[:, w], a.times, theta[:, w], rtol=1e-13, atol=1e-13)
+        tight = cpu_ref.odeint_traj(ode, y0[:, w], a.times, theta[:, w], rtol=1e-13, atol=1e-13)
         np.testing.assert_allclose(rb["traj"][:, :, w], tight, rtol=1e-6, atol=1e-4)

@@ -87,6 +87,27 @@ def pooled(y, t, ps):
     return d
 
 
+def vec_chain(y, t, ps):
+    """The chain model in numpy slice style (whole-array arithmetic, slice assignment)."""
+    mu, phi, beta, lam, tau = ps
+    inf = phi * y[0] * y[-1]
+    dy = np.empty_like(y)
+    dy[0] = mu * y[0] - inf
+    dy[1] = inf - tau * y[1]
+    dy[2:-2] = tau * y[1:-3] - tau * y[2:-2]
+    dy[-2] = tau * y[-3] - lam * y[-2]
+    dy[-1] = beta * lam * y[-2] - inf
+    return dy
+
+
+def vec_misc(y, t, ps):
+    k = np.array([ps[0], ps[1]] + [ps[0] * ps[1]] * (len(y) - 2))
+    out = -k * y + np.exp(-y / 10.0) * t
+    out[1:] += 0.5 * y[:-1] ** 2
+    out *= 1.5
+    return out
+
+
 @pytest.mark.parametrize("n", [4, 7, 8, 12, 20, 33])
 def test_loops_arrays_and_sums_translate_exactly(n):
     """Unrolled loops, local arrays and sums keep Python's operation order: the
@@ -94,6 +115,8 @@ def test_loops_arrays_and_sums_translate_exactly(n):
     order: sequential below 8 elements, 8 strided accumulators above)."""
     tr = transpile(chain_loop, n, 5)
     tp = transpile(pooled, n, 2)
+    tv = transpile(vec_chain, n, 5)
+    tm = transpile(vec_misc, n, 2)
     rs = np.random.RandomState(n)
     for _ in range(25):
         y = rs.uniform(0, 1, n) * 10.0 ** rs.uniform(-3, 7, n)
@@ -101,6 +124,8 @@ def test_loops_arrays_and_sums_translate_exactly(n):
         t = rs.uniform(0, 3)
         assert np.array_equal(tr.evaluate(y, t, ps), chain_loop(y, t, ps))
         assert np.array_equal(tp.evaluate(y, t, ps[:2]), pooled(y, t, ps[:2]))
+        assert np.array_equal(tv.evaluate(y, t, ps), vec_chain(y, t, ps))
+        assert np.array_equal(tm.evaluate(y, t, ps[:2]), vec_misc(y, t, ps[:2]))
     assert "for" not in tr.c_body and f"dy[{n - 1}]" in tr.c_body
 
 
