@@ -8,7 +8,8 @@ subset:
 
 * statements: assignments (also tuple unpacking ``a, b = ps[0], ps[1]`` / ``S, V = y``),
   augmented assignments, docstrings, ``for i in range(...)`` loops with bounds known at
-  translation time (unrolled), local arrays (``dy = np.zeros(len(y))`` /
+  translation time (unrolled), ``if``/``elif``/``else`` on translation-time integers
+  (loop variables, ``len()``; the branch is chosen while translating), local arrays (``dy = np.zeros(len(y))`` /
   ``np.zeros_like(y)`` / ``np.empty(n)`` / ``[0.0] * n`` / a list literal) written and
   read element-wise (``dy[i] = ...``, ``dy[i] += ...``) or by slice (``dy[2:-2] = ...``,
   ``out[1:] += ...``, ``out *= ...``), one final ``return`` of ``np.array([...])``, a
@@ -481,12 +482,32 @@ class _Translator:
                     raise Unsupported("augmented assignment target")
             elif isinstance(st, ast.For):
                 self.unroll(st)
+            elif isinstance(st, ast.If):
+                # a condition on translation-time integers (loop variables, len()) picks
+                # one branch; a condition on data is not supported (use `a if c else b`)
+                self.block(st.body if self.static_cond(st.test) else st.orelse)
             elif isinstance(st, ast.Return):
                 self.outs = self.returned(st.value)
             elif isinstance(st, ast.Pass):
                 continue
             else:
                 raise Unsupported(type(st).__name__)
+
+    _ICMP = {ast.Eq: lambda a, b: a == b, ast.NotEq: lambda a, b: a != b, ast.Lt: lambda a, b: a < b,
+             ast.LtE: lambda a, b: a <= b, ast.Gt: lambda a, b: a > b, ast.GtE: lambda a, b: a >= b}
+
+    def static_cond(self, n):
+        if isinstance(n, ast.Compare) and all(type(o) in self._ICMP for o in n.ops):
+            vals = [self.intexpr(n.left)] + [self.intexpr(c) for c in n.comparators]
+            return all(self._ICMP[type(o)](a, b) for o, a, b in zip(n.ops, vals, vals[1:]))
+        if isinstance(n, ast.BoolOp):
+            parts = [self.static_cond(v) for v in n.values]
+            return all(parts) if isinstance(n.op, ast.And) else any(parts)
+        if isinstance(n, ast.UnaryOp) and isinstance(n.op, ast.Not):
+            return not self.static_cond(n.operand)
+        if isinstance(n, ast.Constant) and isinstance(n.value, bool):
+            return n.value
+        raise Unsupported("`if` on data (only conditions on loop variables / len() / integer constants)")
 
     def unroll(self, st):
         it = st.iter

@@ -75,6 +75,26 @@ def chain_loop(y, t, ps):
     return dy
 
 
+def chain_branchy(y, t, ps):
+    """The chain model with the boundary compartments picked by `if` on the loop index."""
+    mu, phi, beta, lam, tau = ps
+    n = len(y)
+    inf = phi * y[0] * y[n - 1]
+    out = [0.0] * n
+    for k in range(n):
+        if k == 0:
+            out[k] = mu * y[0] - inf
+        elif k == 1:
+            out[k] = inf - tau * y[1]
+        elif k < n - 2:
+            out[k] = tau * y[k - 1] - tau * y[k]
+        elif k == n - 2 and not n < 4:
+            out[k] = tau * y[k - 1] - lam * y[k]
+        else:
+            out[k] = beta * lam * y[n - 2] - inf
+    return out
+
+
 def pooled(y, t, ps):
     """Sums over slices (built-in sum and numpy's pairwise np.sum), augmented element
     updates and a loop variable used as a number."""
@@ -117,6 +137,7 @@ def test_loops_arrays_and_sums_translate_exactly(n):
     tp = transpile(pooled, n, 2)
     tv = transpile(vec_chain, n, 5)
     tm = transpile(vec_misc, n, 2)
+    tb = transpile(chain_branchy, n, 5)
     rs = np.random.RandomState(n)
     for _ in range(25):
         y = rs.uniform(0, 1, n) * 10.0 ** rs.uniform(-3, 7, n)
@@ -126,6 +147,7 @@ def test_loops_arrays_and_sums_translate_exactly(n):
         assert np.array_equal(tp.evaluate(y, t, ps[:2]), pooled(y, t, ps[:2]))
         assert np.array_equal(tv.evaluate(y, t, ps), vec_chain(y, t, ps))
         assert np.array_equal(tm.evaluate(y, t, ps[:2]), vec_misc(y, t, ps[:2]))
+        assert np.array_equal(tb.evaluate(y, t, ps), np.array(chain_branchy(y, t, ps)))
     assert "for" not in tr.c_body and f"dy[{n - 1}]" in tr.c_body
 
 
@@ -143,7 +165,12 @@ def test_unsupported_constructs_are_rejected():
     def wrong_len(y, t, ps):
         return [y[0]]
 
-    for f, S in ((loop, 2), (dyn_index, 1), (wrong_len, 2)):
+    def data_if(y, t, ps):
+        if y[0] > 1.0:
+            return [-y[0]]
+        return [y[0]]
+
+    for f, S in ((loop, 2), (dyn_index, 1), (wrong_len, 2), (data_if, 1)):
         with pytest.raises(Unsupported):
             transpile(f, S, 1)
     with pytest.raises(Unsupported):
