@@ -8,8 +8,10 @@ subset:
 
 * statements: assignments (also tuple unpacking ``a, b = ps[0], ps[1]`` / ``S, V = y``),
   augmented assignments, docstrings, ``for i in range(...)`` loops with bounds known at
-  translation time (unrolled), ``if``/``elif``/``else`` on translation-time integers
-  (loop variables, ``len()``; the branch is chosen while translating), local arrays (``dy = np.zeros(len(y))`` /
+  translation time (unrolled), ``if``/``elif``/``else`` — on translation-time integers
+  (loop variables, ``len()``) the branch is chosen while translating, on data both
+  branches are evaluated and every variable / array element they assign is selected
+  (``cond ? a : b``; no ``return`` inside such a branch) —, local arrays (``dy = np.zeros(len(y))`` /
   ``np.zeros_like(y)`` / ``np.empty(n)`` / ``[0.0] * n`` / a list literal) written and
   read element-wise (``dy[i] = ...``, ``dy[i] += ...``) or by slice (``dy[2:-2] = ...``,
   ``out[1:] += ...``, ``out *= ...``), one final ``return`` of ``np.array([...])``, a
@@ -59,7 +61,7 @@ _CALLS = {
 }
 _MODULES = {"np", "numpy", "math"}
 _CMP = {ast.Lt: ("<", np.less), ast.LtE: ("<=", np.less_equal), ast.Gt: (">", np.greater),
-        ast.GtE: (">=", np.greater_equal)}
+        ast.GtE: (">=", np.greater_equal), ast.Eq: ("==", np.equal), ast.NotEq: ("!=", np.not_equal)}
 
 
 def _c_float(x: float) -> str:
@@ -123,6 +125,12 @@ def _eval(e, y, t, ps, env):
         return _eval(e[2], y, t, ps, env) if _eval(e[1], y, t, ps, env) else _eval(e[3], y, t, ps, env)
     if k == "cmp":
         return bool(_CMP[e[1]][1](_eval(e[2], y, t, ps, env), _eval(e[3], y, t, ps, env)))
+    if k == "and":
+        return all(_eval(a, y, t, ps, env) for a in e[1])
+    if k == "or":
+        return any(_eval(a, y, t, ps, env) for a in e[1])
+    if k == "not":
+        return not _eval(e[1], y, t, ps, env)
     raise AssertionError(k)
 
 
@@ -152,6 +160,9 @@ class _Translator:
         self.outs = None
         self.ints = {}      # translation-time integers: loop variables, len(...), integer locals
         self.arrays = {}    # local arrays: name -> [element variable name or None (unset)]
+        self.scopes = []    # branches of an `if` on data being translated: name -> fresh variable
+        self.uid = 0
+        self.constvals = {}  # float locals currently bound to a numeric literal (usable as indices)
 
     # ---- translation-time integers (indices, loop bounds) ----
     def length_of(self, name):
@@ -171,6 +182,8 @@ class _Translator:
                 return self.ints[n.id]
             if n.id in self.consts and float(self.consts[n.id]).is_integer() and n.id not in self.env:
                 return int(self.consts[n.id])
+            if n.id in self.constvals and float(self.constvals[n.id]).is_integer() and not self.scopes:
+                return int(self.constvals[n.id])
             raise Unsupported(f"{n.id!r} is not an integer known at translation time")
         if isinstance(n, ast.Call) and isinstance(n.func, ast.Name) and n.func.id == "len" and len(n.args) == 1 \
                 and isinstance(n.args[0], ast.Name):
@@ -186,6 +199,16 @@ class _Translator:
             if type(n.op) in ops:
                 return ops[type(n.op)]()
         raise Unsupported("integer expression")
+
+    def int_sourced(self, n):
+        """The expression derives from len() / int() / a translation-time integer (a bare
+        numeric literal stays a float local, usable as an index while it holds it)."""
+        for sub in ast.walk(n):
+            if isinstance(sub, ast.Call) and isinstance(sub.func, ast.Name) and sub.func.id in ("len", "int"):
+                return True
+            if isinstance(sub, ast.Name) and sub.id in self.ints:
+                return True
+        return False
 
     def is_int(self, n):
         """True for an integer expression known at translation time (no y/ps/t data)."""
@@ -301,8 +324,8 @@ class _Translator:
         if isinstance(n, ast.Name):
             if n.id in self.arrays:
                 raise Unsupported(f"array {n.id!r} used as a scalar")
-            if n.id in self.env:
-                return ("var", n.id)
+            if self.defined(n.id):
+                return ("var", self.lookup(n.id))
             if n.id in self.ints:
                 return ("const", float(self.ints[n.id]))
             if n.id == self.tname:
@@ -397,8 +420,14 @@ class _Translator:
         return acc
 
     def cond(self, n):
-        if isinstance(n, ast.Compare) and len(n.ops) == 1 and type(n.ops[0]) in _CMP:
-            return ("cmp", type(n.ops[0]), self.expr(n.left), self.expr(n.comparators[0]))
+        if isinstance(n, ast.Compare) and all(type(o) in _CMP for o in n.ops):
+            terms = [self.expr(n.left)] + [self.expr(c) for c in n.comparators]
+            parts = [("cmp", type(o), a, b) for o, a, b in zip(n.ops, terms, terms[1:])]
+            return parts[0] if len(parts) == 1 else ("and", parts)
+        if isinstance(n, ast.BoolOp):
+            return ("and" if isinstance(n.op, ast.And) else "or", [self.cond(v) for v in n.values])
+        if isinstance(n, ast.UnaryOp) and isinstance(n.op, ast.Not):
+            return ("not", self.cond(n.operand))
         raise Unsupported("condition")
 
     def seq(self, node, n_targets):
@@ -441,8 +470,9 @@ class _Translator:
                         self.new_array(tgt.id, arr)
                     elif tgt.id in self.arrays:
                         raise Unsupported(f"array {tgt.id!r} reassigned")
-                    elif tgt.id not in self.env and self.is_int(st.value):
-                        self.ints[tgt.id] = self.intexpr(st.value)  # e.g. n = len(y)
+                    elif tgt.id not in self.env and not self.scopes and self.is_int(st.value) \
+                            and self.int_sourced(st.value):
+                        self.ints[tgt.id] = self.intexpr(st.value)  # e.g. n = len(y), j = i + 1
                     else:
                         self.ints.pop(tgt.id, None)
                         self.assign([tgt.id], [self.expr(st.value)])
@@ -465,8 +495,8 @@ class _Translator:
                 elif isinstance(st.target, ast.Name) and st.target.id in self.ints:
                     old = ("const", float(self.ints.pop(st.target.id)))
                     self.assign([st.target.id], [("bin", op, old, self.expr(st.value))])
-                elif isinstance(st.target, ast.Name) and st.target.id in self.env and st.target.id not in self.arrays:
-                    self.assign([st.target.id], [("bin", op, ("var", st.target.id), self.expr(st.value))])
+                elif isinstance(st.target, ast.Name) and self.defined(st.target.id) and st.target.id not in self.arrays:
+                    self.assign([st.target.id], [("bin", op, ("var", self.lookup(st.target.id)), self.expr(st.value))])
                 elif isinstance(st.target, ast.Subscript) and isinstance(st.target.value, ast.Name) \
                         and st.target.value.id in self.arrays and isinstance(st.target.slice, ast.Slice):
                     self.set_slice(st.target, lambda old, new, op=op: ("bin", op, old, new), st.value)
@@ -483,9 +513,17 @@ class _Translator:
             elif isinstance(st, ast.For):
                 self.unroll(st)
             elif isinstance(st, ast.If):
-                # a condition on translation-time integers (loop variables, len()) picks
-                # one branch; a condition on data is not supported (use `a if c else b`)
-                self.block(st.body if self.static_cond(st.test) else st.orelse)
+                # a condition on translation-time integers (loop variables, len()) picks one
+                # branch while translating; a condition on data evaluates both branches
+                # and selects every variable / element either branch assigns
+                try:
+                    static = self.static_cond(st.test)
+                except Unsupported:
+                    static = None
+                if static is None:
+                    self.data_if(st)
+                else:
+                    self.block(st.body if static else st.orelse)
             elif isinstance(st, ast.Return):
                 self.outs = self.returned(st.value)
             elif isinstance(st, ast.Pass):
@@ -495,6 +533,47 @@ class _Translator:
 
     _ICMP = {ast.Eq: lambda a, b: a == b, ast.NotEq: lambda a, b: a != b, ast.Lt: lambda a, b: a < b,
              ast.LtE: lambda a, b: a <= b, ast.Gt: lambda a, b: a > b, ast.GtE: lambda a, b: a >= b}
+
+    def defined(self, name):
+        return name in self.env or any(name in d for d in self.scopes)
+
+    def lookup(self, name):
+        for d in reversed(self.scopes):
+            if name in d:
+                return d[name]
+        return name
+
+    def data_if(self, st):
+        cond = self.cond(st.test)
+        before_arrays = {k: list(v) for k, v in self.arrays.items()}
+        before_ints = dict(self.ints)
+        results = []
+        for body in (st.body, st.orelse):
+            self.arrays = {k: list(v) for k, v in before_arrays.items()}
+            self.scopes.append({})
+            self.block(body)
+            names = self.scopes.pop()
+            if self.outs is not None:
+                raise Unsupported("return inside an `if` on data")
+            if self.ints != before_ints or set(self.arrays) != set(before_arrays):
+                raise Unsupported("an `if` on data may only assign floats and array elements")
+            results.append((names, self.arrays))
+        (tn, ta), (en, ea) = results
+        self.arrays = {k: list(v) for k, v in before_arrays.items()}
+        for name in sorted(set(tn) | set(en)):
+            if (name not in tn or name not in en) and not self.defined(name):
+                raise Unsupported(f"{name!r} is assigned in only one branch of an `if` on data")
+            a = tn.get(name, self.lookup(name))
+            b = en.get(name, self.lookup(name))
+            self.assign([name], [("ifexp", cond, ("var", a), ("var", b))])
+        for arr, elems in before_arrays.items():
+            for k, orig in enumerate(elems):
+                a, b = ta[arr][k], ea[arr][k]
+                if a == orig and b == orig:
+                    continue
+                if a is None or b is None:
+                    raise Unsupported(f"{arr}[{k}] is set in only one branch of an `if` on data")
+                self.arrays[arr][k] = self.bind(f"{arr}__{k}", ("ifexp", cond, ("var", a), ("var", b)))
 
     def static_cond(self, n):
         if isinstance(n, ast.Compare) and all(type(o) in self._ICMP for o in n.ops):
@@ -584,11 +663,22 @@ class _Translator:
         self.arrays[name][k] = self.bind(f"{name}__{k}", e)
 
     def bind(self, var, e):
+        if self.scopes:  # inside a branch of an `if` on data: never overwrite a live value
+            var = f"{var}__b{self.uid}"
+            self.uid += 1
         self.stmts.append((var, e))
         self.env.add(var)
         return var
+
     def assign(self, names, exprs):
         if len(names) == 1:
+            if exprs[0][0] == "const" and not self.scopes:
+                self.constvals[names[0]] = exprs[0][1]
+            else:
+                self.constvals.pop(names[0], None)
+            if self.scopes:
+                self.scopes[-1][names[0]] = self.bind(names[0], exprs[0])
+                return
             self.stmts.append((names[0], exprs[0]))
             self.env.add(names[0])
             return
@@ -599,8 +689,7 @@ class _Translator:
             self.env.add(tmp)
             tmps.append(tmp)
         for name, tmp in zip(names, tmps):
-            self.stmts.append((name, ("var", tmp)))
-            self.env.add(name)
+            self.assign([name], [("var", tmp)])
 
     def returned(self, v):
         if isinstance(v, ast.Call) and isinstance(v.func, ast.Attribute) and isinstance(v.func.value, ast.Name) \
@@ -644,6 +733,10 @@ def _c(e) -> str:
         return f"({_c(e[1])} ? {_c(e[2])} : {_c(e[3])})"
     if k == "cmp":
         return f"({_c(e[2])} {_CMP[e[1]][0]} {_c(e[3])})"
+    if k in ("and", "or"):
+        return "(" + (" && " if k == "and" else " || ").join(_c(a) for a in e[1]) + ")"
+    if k == "not":
+        return f"(!{_c(e[1])})"
     raise AssertionError(k)
 
 

@@ -95,6 +95,39 @@ def chain_branchy(y, t, ps):
     return out
 
 
+def thresholds(y, t, ps):
+    """`if`/`elif`/`else` on data (evaluated as selects), a literal local reused as an
+    index, and array elements set in both branches."""
+    a, b = ps
+    x = 0
+    if y[0] < 1.0 and t > 0.5:
+        x = y[0] * a
+        f = 2.0
+    elif y[1] > 3.0 or not y[0] < 2.0:
+        f = b
+    else:
+        f = a * b
+        x += 1.5
+    out = np.zeros(2)
+    out[0] = -f * y[0] + x
+    if 0.0 < y[1] <= 4.0:
+        out[1] = y[1] * f
+    else:
+        out[1] = -y[1]
+    i = 1
+    out[i] += 0.25
+    return out
+
+
+def test_if_on_data_translates_to_selects():
+    tr = transpile(thresholds, 2, 2)
+    assert "?" in tr.c_body and "&&" in tr.c_body and "||" in tr.c_body
+    rs = np.random.RandomState(5)
+    for _ in range(3000):
+        y, t, ps = rs.uniform(0, 5, 2), rs.uniform(0, 1), rs.uniform(0, 1, 2)
+        assert np.array_equal(tr.evaluate(y, t, ps), thresholds(y, t, ps))
+
+
 def pooled(y, t, ps):
     """Sums over slices (built-in sum and numpy's pairwise np.sum), augmented element
     updates and a loop variable used as a number."""
@@ -190,5 +223,7 @@ def test_resolution_prefers_builtins_then_rtc():
 
 def test_transpiled_rhs_compiles_with_hiprtc_for_gfx950():
     N.rtc_check(transpile(sat_infection, 2, 4).c_body, 2, 4, "gfx950")
+    N.rtc_check(transpile(vec_misc, 6, 2).c_body, 6, 2, "gfx950")
+    N.rtc_check(transpile(thresholds, 2, 2).c_body, 2, 2, "gfx950")
     with pytest.raises(ValueError, match="hipRTC compilation"):
         N.rtc_check("dy[0] = no_such_symbol;", 1, 1, "gfx950")
