@@ -36,8 +36,8 @@ FP64_VALU_TFS = 78.6     # MI355X FP64 vector spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
     ap.add_argument("--model", default="two_i", help="two_i | chain<N>")
     ap.add_argument("--method", default="rk4", choices=["rk4", "dopri5"])
@@ -330,9 +330,9 @@ def main():
             y0t = torch.as_tensor(np.repeat(y0x[:, None], W, axis=1), device=dev).contiguous()
             trx = ex.empty_traj(W)
             ms = []
-            for r in range(7):
+            for r in range(15):  # 5 untimed launches (clocks and caches settle), median of 10
                 ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True)
-                if r >= 2:
+                if r >= 5:
                     ms.append(ex.last_kernel_ms())
             kms = float(np.median(ms))
             byt = W * (T - 1) * 8 * Sx
