@@ -85,8 +85,7 @@ enum {
   OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel (opt-in, S <= 8, W even) */
   OE_HALF_WAVES = 16u, /* RK4: 32 walkers per wavefront (twice the waves; same results). Chosen
                          automatically for trajectories with S >= 5 at <= 1 wave per SIMD. */
-  OE_SPLIT_WAVES = 32u, /* trajectories: two wavefronts integrate the same 64 walkers and each
-                          stores half of the states (twice the storing waves; same results) */
+  /* 32u: reserved (was an experimental split-wave layout, measured slower and removed) */
   OE_NO_XCD_REMAP = 64u /* oe_integrate: keep blockIdx-order walker blocks.  By default the
                            blocks an XCD receives (round-robin dispatch) take one contiguous
                            range of walkers (same results, faster trajectory stores) */

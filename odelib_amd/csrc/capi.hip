@@ -462,9 +462,8 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     // groups (its step size is shared per wave).
     const bool rk4 = c->method == OE_METHOD_RK4;
     const bool auto_half = rk4 && ia.traj && S >= 5 && W <= (int64_t)64 * 4 * c->n_cu;
-    ia.split = (ia.traj && (flags & OE_SPLIT_WAVES) && S >= 2) ? 1 : 0;
-    ia.half = (!ia.split && rk4 && ((flags & OE_HALF_WAVES) || auto_half)) ? 1 : 0;
-    const int64_t per_block = (ia.half || ia.split) ? kBlock / 2 : kBlock;
+    ia.half = (rk4 && ((flags & OE_HALF_WAVES) || auto_half)) ? 1 : 0;
+    const int64_t per_block = ia.half ? kBlock / 2 : kBlock;
     const dim3 grid((unsigned)((W + per_block - 1) / per_block)), block(kBlock);
     ia.xcd_remap = (flags & OE_NO_XCD_REMAP) ? 0 : 1;
     OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));

@@ -151,27 +151,16 @@ __device__ __forceinline__ void check_finite(const double (&y)[S], Acc& a) {
 // Store grid row i of the trajectory (TRAJ) and track the minimum state.  `off` is
 // the lane's byte offset w*8 (32-bit); rows are stored through a per-row buffer
 // descriptor (S*W*8 < 2^32, checked on the host): no per-store VALU address math.
-// `sp` (wave-uniform) selects the states this wave stores: -1 all of them; with split
-// waves (two waves integrate the same 64 walkers) 0 the lower half [0, S/2), 1 the upper.
 template <int S, bool TRAJ, bool NT>
 __device__ __forceinline__ void store_row(int i, const double (&y)[S], double* __restrict__ traj,
-                                          int64_t W, uint32_t off, bool active, Acc& a, int sp) {
+                                          int64_t W, uint32_t off, bool active, Acc& a) {
   if constexpr (TRAJ) {
     if (active) {
       const uint32_t row_bytes = (uint32_t)(S * W * 8);
       const __amdgpu_buffer_rsrc_t rsrc =
           __builtin_amdgcn_make_buffer_rsrc((void*)(traj + (int64_t)i * S * W), 0, row_bytes, 0x00020000);
-      constexpr int H = S / 2;
-      if (sp < 0) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
-      } else if (sp == 0) {
-#pragma unroll
-        for (int s = 0; s < H; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
-      } else {
-#pragma unroll
-        for (int s = H; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
-      }
+      for (int s = 0; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
     }
   }
 #pragma unroll
@@ -219,8 +208,8 @@ __device__ __forceinline__ void observe_next(const DevProblem& pb, int i, const 
 template <int S, bool TRAJ, bool NT, bool INLINE_LOG = false>
 __device__ __forceinline__ void emit(const DevProblem& pb, int i, const double (&y)[S],
                                      double* __restrict__ traj, int64_t W, uint32_t off,
-                                     bool active, int& k, Acc& a, int sp) {
-  store_row<S, TRAJ, NT>(i, y, traj, W, off, active, a, sp);
+                                     bool active, int& k, Acc& a) {
+  store_row<S, TRAJ, NT>(i, y, traj, W, off, active, a);
   observe<S, INLINE_LOG>(pb, i, y, k, a);
 }
 
@@ -260,9 +249,9 @@ __device__ __forceinline__ void rk4_step(double (&y)[M::S], double t, double h, 
 template <class M, int PMAX, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[M::S],
                                               const double (&p)[PMAX], double* traj,
-                                              int64_t W, uint32_t off, bool active, Acc& a, int sp) {
+                                              int64_t W, uint32_t off, bool active, Acc& a) {
   int k = 0;
-  emit<M::S, TRAJ, NT, TRAJ>(pb, 0, y, traj, W, off, active, k, a, sp);
+  emit<M::S, TRAJ, NT, TRAJ>(pb, 0, y, traj, W, off, active, k, a);
   const int n = pb.substeps;
   const cptr<double> tab = kconst(pb.rk4);
   const cptr<Obs> obs = kconst(pb.obs);
@@ -284,11 +273,11 @@ __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[
     const int next = (k < pb.n_obs) ? obs[k].tidx : pb.T;
     for (; i < next; ++i) {
       interval(i);
-      if constexpr (TRAJ) store_row<M::S, TRAJ, NT>(i, y, traj, W, off, active, a, sp);
+      if constexpr (TRAJ) store_row<M::S, TRAJ, NT>(i, y, traj, W, off, active, a);
     }
     if (i < pb.T) {  // i == next: an observed grid point
       interval(i);
-      emit<M::S, TRAJ, NT, TRAJ>(pb, i, y, traj, W, off, active, k, a, sp);
+      emit<M::S, TRAJ, NT, TRAJ>(pb, i, y, traj, W, off, active, k, a);
       ++i;
     }
   }
@@ -347,11 +336,11 @@ __device__ __forceinline__ double inv_fifth_root(double x) {
 template <class M, int PMAX, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
-                                                 int64_t W, uint32_t off, bool active, Acc& a, int sp) {
+                                                 int64_t W, uint32_t off, bool active, Acc& a) {
   using namespace dp;
   constexpr int S = M::S;
   int k = 0;
-  emit<S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a, sp);
+  emit<S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
   const cptr<double> times = kconst(pb.times);
   const double t0 = times[0];
   const double tend = times[pb.T - 1];
@@ -506,10 +495,10 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
               for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
             }
-            emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a, sp);
+            emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
           } else {
             // (an evicted lane's state is NaN, so its dense output is NaN already)
-            store_row<S, TRAJ, NT>(i, yo, traj, W, off, active, a, sp);
+            store_row<S, TRAJ, NT>(i, yo, traj, W, off, active, a);
             if (i == nxt) {
               observe_next<S>(pb, i, yo, k, nxt, a);
               t_obs = (nxt < pb.T) ? times[nxt] : __builtin_inf();
@@ -549,7 +538,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
         for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
         for (; i < pb.T; ++i)
-          if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a, sp);
+          if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
         break;
       }
       if (h < hmin) h = fmin(1e-3 * span, tend - t);
@@ -563,10 +552,10 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
 template <class M, int PMAX, int METHOD, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
-                                                 int64_t W, int64_t w, bool active, Acc& a, int sp = -1) {
+                                                 int64_t W, int64_t w, bool active, Acc& a) {
   const uint32_t off = (uint32_t)w * 8u;  // byte offset of walker w in a [..][W] row
-  if constexpr (METHOD == 0) integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a, sp);
-  else integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a, sp);
+  if constexpr (METHOD == 0) integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  else integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
 }
 
 // ---------------------------------------------------------------------------------
@@ -581,7 +570,6 @@ struct IntegrateArgs {
   double* ssres;        // [W] or null
   int32_t* status;      // [W] or null
   int32_t half;         // 1: 32 walkers per wavefront (lanes 32-63 idle), 0: 64
-  int32_t split;        // 1: two waves integrate the same 64 walkers, each stores half the states
   int32_t xcd_remap;    // 1: the blocks dispatched to XCD x (blockIdx % 8, round-robin) take the
                         //    x-th contiguous range of walker blocks (xcd_block)
 };
@@ -607,19 +595,11 @@ __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const In
   const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   int64_t gw = blk * blockDim.x + threadIdx.x;
   bool idle = false;
-  int sp = -1;
   if (ia.half) {  // walker = (wave, lane < 32); the upper half-wave idles (DOPRI5: dead lanes)
     const int lane = threadIdx.x & 63;
     gw = (blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32 + (lane & 31);
     idle = lane >= 32;
     if (METHOD == 0 && idle) return;
-  } else if (ia.split) {
-    // waves 2g and 2g+1 of a block run walker group g (64 walkers) redundantly; the even
-    // wave stores states [0, S/2), the odd one [S/2, S): twice the storing waves at the
-    // same store-instruction count, compute duplicated (it is hidden under the stores)
-    const int wv = threadIdx.x >> 6;
-    gw = (blk * (blockDim.x >> 7) + (wv >> 1)) * 64 + (threadIdx.x & 63);
-    sp = __builtin_amdgcn_readfirstlane(wv & 1);
   }
   const bool active = gw < ia.W && !idle;
   const int64_t w = gw < ia.W ? gw : ia.W - 1;  // tail lanes shadow the last walker, never store
@@ -630,8 +610,8 @@ __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const In
 #pragma unroll
   for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
   Acc a = acc_init();
-  integrate_walker<M, PMAX, METHOD, TRAJ, NT>(pb, y, p, ia.traj, W, w, active, a, sp);
-  if (active && sp <= 0) {
+  integrate_walker<M, PMAX, METHOD, TRAJ, NT>(pb, y, p, ia.traj, W, w, active, a);
+  if (active) {
     if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
     if (ia.ssres) ia.ssres[w] = a.ssres;
     if (ia.status) ia.status[w] = finish(a);

@@ -100,20 +100,17 @@ def test_rk4_half_waves_match_full_waves(spec, W):
 @pytest.mark.parametrize("method", ["rk4", "dopri5"])
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain5", "chain20"])
 @pytest.mark.parametrize("W", [1, 100, 4099, 8192])
-def test_split_waves_match_full_waves(method, spec, W):
-    """Two wavefronts per 64 walkers, each storing half of the states (OE_SPLIT_WAVES),
-    give the bits of the one-wave layout (trajectory, chi, R² residual, status),
-    incl. ragged tails and odd S."""
+def test_xcd_block_order_matches_blockidx_order(method, spec, W):
+    """XCD-contiguous walker blocks (the default) give the bits of blockIdx-order blocks
+    (trajectory, chi, R² residual, status), incl. ragged tails and odd S."""
     m = _model(spec, method)
     theta = _walkers(spec, W)
     y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
     eng = m.engine()
-    a = eng.integrate(y0, theta, split_waves=True)
-    b = eng.integrate(y0, theta, half_waves=False)
-    c = eng.integrate(y0, theta, xcd_remap=False)  # blockIdx-order walker blocks
+    a = eng.integrate(y0, theta)
+    c = eng.integrate(y0, theta, xcd_remap=False)
     for key in ("traj", "chi", "ssres", "status"):
-        assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
-        assert np.array_equal(c[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
+        assert np.array_equal(c[key].cpu().numpy(), a[key].cpu().numpy(), equal_nan=True), key
 
 
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain8"])

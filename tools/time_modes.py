@@ -31,14 +31,14 @@ def main():
         y0 = torch.as_tensor(np.repeat(y0h[:, None], W, axis=1), device=dev).contiguous()
         traj = eng.empty_traj(W)
         row = {"case": case}
-        modes = ("traj", "notraj", "traj_half", "traj_split", "traj_noxcd")
+        modes = ("traj", "notraj", "traj_half", "traj_noxcd")
         ms = {k: [] for k in modes}
         # interleaved rounds after a warm-up of every mode (clocks settle, pages mapped)
         for r in range(args.reps + 3):
             for mode in modes:
                 eng.integrate(y0, theta, trajectory=mode.startswith("traj"),
                               traj_out=traj if mode.startswith("traj") else None, sync=True,
-                              half_waves=mode.endswith("half"), split_waves=mode.endswith("split"),
+                              half_waves=mode.endswith("half"),
                               xcd_remap=not mode.endswith("noxcd"))
                 if r >= 3:
                     ms[mode].append(eng.last_kernel_ms())
