@@ -340,6 +340,33 @@ def test_mh_replay_and_state0_params_vs_c_restatement():
     np.testing.assert_allclose(dev["y0"].cpu().numpy()[2], dev["theta"].cpu().numpy()[4], rtol=0)
 
 
+@pytest.mark.parametrize("method", ["rk4", "dopri5"])
+@pytest.mark.parametrize("T", [2, 3, 17])
+def test_short_grids_bitwise_vs_c_restatement(method, T):
+    """Grids of 2, 3 and 17 output times (every observation folded onto few rows; the
+    DOPRI5 step spans many rows or ends exactly on the last one) — same bits as C."""
+    from helpers import chain_problem
+    m = chain_problem(4, method=method, T=T)
+    theta = _walkers("chain4", 70)
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"])
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
+    assert np.array_equal(out["status"], ref["status"])
+
+
+@pytest.mark.parametrize("method", ["rk4", "dopri5"])
+def test_mh_all_parameters_static_vs_c_restatement(method):
+    """static_parameters = every parameter: the chains never move, every proposal is
+    the current state (accepted: exp(0) > u), samples repeat it — as in the C oracle."""
+    m, P, theta, y0 = _mh_inputs("two_i", 70, method)
+    walk = np.zeros(P, np.uint8)
+    dev = m.engine().mh_run(theta, y0, nits=8, burnin=2, walk_mask=walk, rng="philox", seed=2)
+    ref = rk_ref.mh_run(m.fit_problem(), theta, y0, 8, 2, walk, rng="philox", seed=2)
+    np.testing.assert_allclose(dev["samples"].cpu().numpy(), ref["samples"], rtol=1e-11)
+    assert np.array_equal(dev["theta"].cpu().numpy(), theta)
+
+
 def test_mh_degenerate_lengths():
     m, P, theta, y0 = _mh_inputs("two_i", 10)
     walk = np.ones(P, np.uint8)
