@@ -309,6 +309,34 @@ constexpr double d1 = -12715105075.0 / 11282082432.0, d3 = 87487479700.0 / 32700
                  d6 = -1453857185.0 / 822651844.0, d7 = 69997945.0 / 29380423.0;
 constexpr double safe = 0.9, facmin = 0.2, facmax = 10.0;
 
+// The tableau as a table in device memory: trajectory kernels (one wave per SIMD, VGPRs
+// to spare) load it once per lane into VGPRs instead of re-materialising each 64-bit
+// constant with two s_mov per use and step.
+__device__ const double kTab[36] = {a21, a31, a32, a41, a42, a43, a51, a52, a53, a54, a61, a62, a63, a64, a65,
+                                    a71, a73, a74, a75, a76, e1, e3, e4, e5, e6, e7, d1, d3, d4, d5, d6, d7,
+                                    c2, c3, c4, c5};
+struct Tab {
+  double v[36];
+};
+template <bool VREG>
+__device__ __forceinline__ Tab load_tab() {
+  Tab t;
+  if constexpr (VREG) {
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // opaque per-lane zero: vector loads, values stay in VGPRs
+    const double* p = kTab + z;
+#pragma unroll
+    for (int j = 0; j < 36; ++j) t.v[j] = p[j];
+  } else {
+    const double c[36] = {a21, a31, a32, a41, a42, a43, a51, a52, a53, a54, a61, a62, a63, a64, a65,
+                          a71, a73, a74, a75, a76, e1, e3, e4, e5, e6, e7, d1, d3, d4, d5, d6, d7,
+                          c2, c3, c4, c5};
+#pragma unroll
+    for (int j = 0; j < 36; ++j) t.v[j] = c[j];
+  }
+  return t;
+}
+
 // x^(-1/5) for finite x > 0 (the step controller's err^(-1/5) and HINIT's
 // (0.01/dm)^(1/5)).  Only exact scalings (frexp/ldexp) and IEEE mul/fma, so the host
 // restatement (oracle/rk_ref.c inv_fifth_root) reproduces it bit for bit — libm's and
@@ -347,6 +375,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
   const double rtol = pb.rtol, atol = pb.atol;
   bool dead = !active;  // dead lanes never enter the wave norm
   double t = t0;
+  const Tab tb = load_tab<TRAJ && (M::S <= 8)>();
   double k1[S], k2[S], k3[S], k4[S], k5[S], k6[S], k7[S], yt[S], yn[S];
   M::rhs(y, t, p, k1);
 
@@ -396,25 +425,25 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
     bool last = false;
     if (t + h >= tend) { h = tend - t; last = true; }
     // h-scaled tableau (wave-uniform), then one fma chain per stage and state
-    const double b21 = h * a21;
-    const double b31 = h * a31, b32 = h * a32;
-    const double b41 = h * a41, b42 = h * a42, b43 = h * a43;
-    const double b51 = h * a51, b52 = h * a52, b53 = h * a53, b54 = h * a54;
-    const double b61 = h * a61, b62 = h * a62, b63 = h * a63, b64 = h * a64, b65 = h * a65;
-    const double b71 = h * a71, b73 = h * a73, b74 = h * a74, b75 = h * a75, b76 = h * a76;
+    const double b21 = h * tb.v[0];
+    const double b31 = h * tb.v[1], b32 = h * tb.v[2];
+    const double b41 = h * tb.v[3], b42 = h * tb.v[4], b43 = h * tb.v[5];
+    const double b51 = h * tb.v[6], b52 = h * tb.v[7], b53 = h * tb.v[8], b54 = h * tb.v[9];
+    const double b61 = h * tb.v[10], b62 = h * tb.v[11], b63 = h * tb.v[12], b64 = h * tb.v[13], b65 = h * tb.v[14];
+    const double b71 = h * tb.v[15], b73 = h * tb.v[16], b74 = h * tb.v[17], b75 = h * tb.v[18], b76 = h * tb.v[19];
 #pragma unroll
     for (int s = 0; s < S; ++s) yt[s] = fma(b21, k1[s], y[s]);
-    M::rhs(yt, t + c2 * h, p, k2);
+    M::rhs(yt, t + tb.v[32] * h, p, k2);
 #pragma unroll
     for (int s = 0; s < S; ++s) yt[s] = fma(b32, k2[s], fma(b31, k1[s], y[s]));
-    M::rhs(yt, t + c3 * h, p, k3);
+    M::rhs(yt, t + tb.v[33] * h, p, k3);
 #pragma unroll
     for (int s = 0; s < S; ++s) yt[s] = fma(b43, k3[s], fma(b42, k2[s], fma(b41, k1[s], y[s])));
-    M::rhs(yt, t + c4 * h, p, k4);
+    M::rhs(yt, t + tb.v[34] * h, p, k4);
 #pragma unroll
     for (int s = 0; s < S; ++s)
       yt[s] = fma(b54, k4[s], fma(b53, k3[s], fma(b52, k2[s], fma(b51, k1[s], y[s]))));
-    M::rhs(yt, t + c5 * h, p, k5);
+    M::rhs(yt, t + tb.v[35] * h, p, k5);
 #pragma unroll
     for (int s = 0; s < S; ++s)
       yt[s] = fma(b65, k5[s], fma(b64, k4[s], fma(b63, k3[s], fma(b62, k2[s], fma(b61, k1[s], y[s])))));
@@ -425,7 +454,8 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
     M::rhs(yn, t + h, p, k7);
     // ---- per-lane max-norm error: argmax of |e_s|/sk_s by exact cross-multiplication,
     //      then ONE division; non-finite anywhere -> 1e30 (forces a reject) ----
-    const double g1 = h * e1, g3 = h * e3, g4 = h * e4, g5 = h * e5, g6 = h * e6, g7 = h * e7;
+    const double g1 = h * tb.v[20], g3 = h * tb.v[21], g4 = h * tb.v[22], g5 = h * tb.v[23], g6 = h * tb.v[24],
+                 g7 = h * tb.v[25];
     double num = 0.0, den = 1.0, nfe = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -454,7 +484,8 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
       constexpr bool kHoist = TRAJ || S <= 8;
       const double rh = 1.0 / h;  // one division per step, not per grid point
       double ydf[kHoist ? S : 1], bsp[kHoist ? S : 1], r4[kHoist ? S : 1], r5[kHoist ? S : 1];
-      const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
+      const double hd1 = h * tb.v[26], hd3 = h * tb.v[27], hd4 = h * tb.v[28], hd5 = h * tb.v[29],
+                   hd6 = h * tb.v[30], hd7 = h * tb.v[31];
       if (kHoist && kEager) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
