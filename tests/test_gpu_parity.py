@@ -535,3 +535,37 @@ def test_fit_survey_and_equilibria():
     eq = m.explore_equilibriums(samples=64)
     assert list(eq.columns) == m.get_snames(after_summation=False) + m.get_pnames()
     assert len(eq) == 64
+
+
+# --------------------------------------------------------------------- C-ABI host pointers
+@pytest.mark.parametrize("method", ["rk4", "dopri5"])
+def test_c_abi_host_pointers_match_device_path(method):
+    """oe_integrate with OE_HOST_PTRS and plain numpy buffers — the binding a maintainer
+    would add to ODElib itself — returns the device path's bits."""
+    import ctypes as C
+    m = _model("two_i", method)
+    W = 300
+    theta = np.ascontiguousarray(_walkers("two_i", W))
+    y0 = np.ascontiguousarray(np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1))
+    fp = m.fit_problem()
+    ctx = N.Context(0)
+    try:
+        ctx.problem_set(fp.to_c())
+        T, S = fp.n_times, fp.n_states
+        traj = np.empty((T, S, W))
+        chi = np.empty(W)
+        ssres = np.empty(W)
+        st = np.empty(W, np.int32)
+        ptr = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+        ctx.integrate(W, ptr(y0), ptr(theta), ptr(traj), ptr(chi), ptr(ssres), ptr(st), N.OE_HOST_PTRS)
+        # without a trajectory buffer (MCMC-style call)
+        chi2 = np.empty(W)
+        ctx.integrate(W, ptr(y0), ptr(theta), None, ptr(chi2), None, None, N.OE_HOST_PTRS)
+    finally:
+        ctx.close()
+    dev = m.engine().integrate(y0, theta)
+    assert np.array_equal(traj, dev["traj"].cpu().numpy())
+    assert np.array_equal(chi, dev["chi"].cpu().numpy(), equal_nan=True)
+    assert np.array_equal(ssres, dev["ssres"].cpu().numpy())
+    assert np.array_equal(st, dev["status"].cpu().numpy())
+    assert np.array_equal(chi2, chi, equal_nan=True)
