@@ -92,13 +92,38 @@ __device__ __forceinline__ double lane63(double v) {
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
   return __hiloint2double(hi, lo);
 }
+// Wave maximum of NON-NEGATIVE, non-NaN values (the DOPRI5 error norm): every DPP hop is
+// a plain mov_dpp with bound_ctrl and all rows enabled (a lane with no source reads 0,
+// neutral for max; a bcast hop that also writes rows 0/2 hands them some in-wave value,
+// which never exceeds the true maximum, and lane 63 still sees every row), and the max is
+// a raw v_max_f64 — no copy for the DPP `old` operand and no canonicalising max of the
+// DPP result: 3 VALU ops per hop instead of 6.  max is exact, so the hop order cannot
+// change the result.
+template <int CTRL>
+__device__ __forceinline__ double dpp0_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double max_raw(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// fmax(|a|, |b|) in one op (the compiler canonicalises one operand first).  Quiet NaN in
+// one operand returns the other, as C fmax does; the kernels never make signalling NaNs.
+__device__ __forceinline__ double max_abs_raw(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ double wave_max(double v) {
-  v = fmax(v, dpp_f64<0xB1>(v));        // quad_perm [1,0,3,2]
-  v = fmax(v, dpp_f64<0x4E>(v));        // quad_perm [2,3,0,1]
-  v = fmax(v, dpp_f64<0x141>(v));       // row_half_mirror
-  v = fmax(v, dpp_f64<0x140>(v));       // row_mirror
-  v = fmax(v, dpp_f64<0x142, 0xA>(v));  // row_bcast15 -> rows 1, 3
-  v = fmax(v, dpp_f64<0x143, 0xC>(v));  // row_bcast31 -> rows 2, 3
+  v = max_raw(v, dpp0_f64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = max_raw(v, dpp0_f64<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = max_raw(v, dpp0_f64<0x141>(v));  // row_half_mirror
+  v = max_raw(v, dpp0_f64<0x140>(v));  // row_mirror
+  v = max_raw(v, dpp0_f64<0x142>(v));  // row_bcast15: row r gets row r-1's maximum
+  v = max_raw(v, dpp0_f64<0x143>(v));  // row_bcast31: rows 2, 3 get rows 0-1's maximum
   return lane63(v);
 }
 __device__ __forceinline__ double wave_min(double v) {
@@ -461,7 +486,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
     for (int s = 0; s < S; ++s) {
       const double e = fma(g7, k7[s], fma(g6, k6[s], fma(g5, k5[s], fma(g4, k4[s], fma(g3, k3[s], g1 * k1[s])))));
       const double ae = fabs(e);
-      const double sk = fma(rtol, fmax(fabs(y[s]), fabs(yn[s])), atol);
+      const double sk = fma(rtol, max_abs_raw(y[s], yn[s]), atol);
       nfe = fma(ae, 0.0, nfe);
       if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
     }
