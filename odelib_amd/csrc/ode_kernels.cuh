@@ -117,6 +117,11 @@ __device__ __forceinline__ double max_abs_raw(double a, double b) {
   asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+__device__ __forceinline__ double min_raw(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ double wave_max(double v) {
   v = max_raw(v, dpp0_f64<0xB1>(v));   // quad_perm [1,0,3,2]
   v = max_raw(v, dpp0_f64<0x4E>(v));   // quad_perm [2,3,0,1]
@@ -188,8 +193,10 @@ __device__ __forceinline__ void store_row(int i, const double (&y)[S], double* _
       for (int s = 0; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
     }
   }
+  // raw v_min_f64 (fmin's canonicalising copies of both operands doubled the VALU count
+  // of the minimum); a quiet NaN operand returns the other, as C fmin does
 #pragma unroll
-  for (int s = 0; s < S; ++s) a.ymin = fmin(a.ymin, y[s]);
+  for (int s = 0; s < S; ++s) a.ymin = min_raw(a.ymin, y[s]);
 }
 
 // Fold every observation recorded at grid index i into the likelihood (caller knows
@@ -735,7 +742,7 @@ __global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevP
 #pragma unroll
       for (int s = 0; s < S; ++s) ring[half][h][s][b] = v[s];
 #pragma unroll
-      for (int s = 0; s < S; ++s) a.ymin = fmin(a.ymin, v[s]);
+      for (int s = 0; s < S; ++s) a.ymin = min_raw(a.ymin, v[s]);
     };
     auto interval = [&](int i) {
       const double h = tab[4 * (i - 1)], hh = tab[4 * (i - 1) + 1], h6 = tab[4 * (i - 1) + 2];
