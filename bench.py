@@ -233,8 +233,11 @@ def main():
     y0 = torch.as_tensor(np.repeat(y0h[:, None], Wl, axis=1), device=dev).contiguous()
     traj = eng.empty_traj(Wl)
 
-    def step():
-        return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores, sync=False)
+    def step(timing=False):
+        # no timing-event markers between the timed launches (measured: markers between
+        # back-to-back launches cost ~4 % of the C1 wall time, tools/launch_gaps.py)
+        return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores,
+                             sync=False, timing=timing)
 
     for _ in range(args.warmup):
         step()
@@ -242,13 +245,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    stream = torch.cuda.current_stream(dev)  # the stream the engine launches on
+    span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
+    span[0].record(stream)
     for k in range(args.steps):
-        ev[k][0].record(stream)
         out = step()
-        ev[k][1].record(stream)
+    span[1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -258,8 +261,18 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    # average launch duration over the timed region: HIP events bracketing the K
+    # back-to-back launches on the launch stream
+    kern_avg_s = span[0].elapsed_time(span[1]) / args.steps / 1e3
+    # per-dispatch durations (event pair around each launch; the rocprofv3 view), in an
+    # untimed pass of the same launches after the timed region
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    kern_dispatch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     wts = n_gpus * Wl * (T - 1) * args.steps
     value = wts / elapsed
     bytes_launch = Wl * (T - 1) * 8 * S + Wl * 8 * (S + P + 2)  # traj + y0/θ/chi/ssres
@@ -357,7 +370,8 @@ def main():
                        "method": args.method, "stores": "cached" if args.cached_stores else "nontemporal", "parallelism": f"walker-shard x{n_gpus}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
-                         "kernel_ms": kern_avg_s * 1e3, "bytes_per_launch": bytes_launch},
+                         "kernel_ms": kern_avg_s * 1e3, "kernel_ms_note": "timed-region event span / steps",
+                         "kernel_ms_per_dispatch": kern_dispatch_ms, "bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "mcmc": mcmc,
             "other_configs": extra,

@@ -86,9 +86,12 @@ enum {
   OE_HALF_WAVES = 16u, /* RK4: 32 walkers per wavefront (twice the waves; same results). Chosen
                          automatically for trajectories with S >= 5 at <= 1 wave per SIMD. */
   /* 32u: reserved (was an experimental split-wave layout, measured slower and removed) */
-  OE_NO_XCD_REMAP = 64u /* oe_integrate: keep blockIdx-order walker blocks.  By default the
+  OE_NO_XCD_REMAP = 64u, /* oe_integrate: keep blockIdx-order walker blocks.  By default the
                            blocks an XCD receives (round-robin dispatch) take one contiguous
                            range of walkers (same results, faster trajectory stores) */
+  OE_NO_TIMING = 128u   /* oe_integrate: record no timing events around the launch (back-to-back
+                           launches without event markers between them); oe_last_kernel_ms
+                           then reports OE_ERR_STATE until a timed call */
 };
 
 /* RNG modes for oe_mh_run */

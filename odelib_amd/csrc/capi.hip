@@ -450,7 +450,8 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   // it is not the default.
   const bool piped = (flags & OE_PIPE) && !e->rtc && c->method == OE_METHOD_RK4 && ia.traj && e->rk4_piped[nt ? 1 : 0] &&
                      (W % 2 == 0);
-  OE_HIP(c, hipEventRecord(c->ev0, c->stream));
+  const bool timing = !(flags & OE_NO_TIMING);
+  if (timing) OE_HIP(c, hipEventRecord(c->ev0, c->stream));
   if (piped) {
     const dim3 grid((unsigned)((W + kPipeWalkers - 1) / kPipeWalkers)), block(kPipeThreads);
     e->rk4_piped[nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
@@ -469,8 +470,8 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));
   }
   OE_HIP(c, hipGetLastError());
-  OE_HIP(c, hipEventRecord(c->ev1, c->stream));
-  c->timed = true;
+  if (timing) OE_HIP(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = timing;
 
   if (host) {
     if (h_traj)

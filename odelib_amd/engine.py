@@ -149,14 +149,15 @@ class Engine:
     # -- batched integrate -------------------------------------------------------------------
     def integrate(self, y0, theta, trajectory: bool = True, traj_out=None, nt_stores: bool = True,
                   sync: bool = True, pipelined: bool = False, half_waves: bool = False,
-                  xcd_remap: bool = True):
+                  xcd_remap: bool = True, timing: bool = True):
         """y0 [S][W], theta [P][W] → dict(traj [T][S][W] | None, chi [W], ssres [W], status [W]).
 
         ``pipelined=True`` selects the opt-in producer/consumer RK4 trajectory kernel
         (same results; not faster on MI355X).  ``half_waves=True`` runs
         32 walkers per wavefront (twice the waves; same results).
         ``xcd_remap=False`` keeps blockIdx-order walker blocks instead of one contiguous
-        walker range per XCD (same results)."""
+        walker range per XCD (same results).  ``timing=False`` records no library events
+        around the launch (``last_kernel_ms`` is then unavailable for this call)."""
         torch = self.torch
         pb = self.problem
         theta_t = theta if isinstance(theta, torch.Tensor) else np.asarray(theta)
@@ -175,7 +176,7 @@ class Engine:
         self._sync_stream()
         flags = N.OE_ASYNC | (N.OE_NT_STORES if nt_stores else 0) | (N.OE_PIPE if pipelined else 0) \
             | (N.OE_HALF_WAVES if half_waves else 0) \
-            | (0 if xcd_remap else N.OE_NO_XCD_REMAP)
+            | (0 if xcd_remap else N.OE_NO_XCD_REMAP) | (0 if timing else N.OE_NO_TIMING)
         self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)
         if sync:
             torch.cuda.synchronize(self.dev)

@@ -95,6 +95,21 @@ def main():
     for r in stats:
         summary["kernels"].append({k: r[k] for k in r})
     summary["bench_line_under_profiler"] = json.loads(bench_line[-1]) if bench_line else None
+    # the bench's timed region alone: the C1 dispatches after the warmup launches and
+    # before the per-dispatch (event-marked) pass, from the kernel trace
+    bl = summary["bench_line_under_profiler"]
+    trace_csv = find(os.path.join(d, "**", "*kernel_trace.csv"))
+    if bl and trace_csv:
+        hot = [r for r in read_csv(trace_csv) if "k_integrate<oe::TwoI, 0, true, true>" in r["Kernel_Name"]]
+        hot.sort(key=lambda r: int(r["Start_Timestamp"]))
+        w, k = bl["warmup"], bl["steps"]
+        timed = hot[w:w + k]
+        if len(timed) == k:
+            durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
+            span = (int(timed[-1]["End_Timestamp"]) - int(timed[0]["Start_Timestamp"])) / 1e6
+            summary["timed_region"] = {"dispatches": k, "mean_dispatch_ms": sum(durs) / k,
+                                       "span_ms_per_dispatch": span / k,
+                                       "bench_event_kernel_ms": bl["roofline"]["kernel_ms"]}
 
     # 2./3. HBM traffic per dispatch of the hot kernel, separate PMC passes
     if not args.skip_pmc:
@@ -113,6 +128,7 @@ def main():
     with open(os.path.join(out, f"{args.tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary.get("pmc"), indent=1))
+    print(json.dumps(summary.get("timed_region"), indent=1))
     for k in summary["kernels"]:
         print({kk: k[kk] for kk in k if kk in ("Name", "Calls", "AverageNs", "TotalDurationNs", "Percentage")})
 
