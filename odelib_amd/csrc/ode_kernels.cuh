@@ -913,6 +913,16 @@ struct Row {
   }
 };
 
+// A uniform pointer the compiler must treat as redefined here: row resources derived
+// from it are rebuilt at their use (a few SALU) instead of hoisted out of the MH
+// iteration loop, where S + 2P hoisted 4-SGPR descriptors (chain20: ~120 SGPRs) stay
+// live across the whole integration and spill to VGPR lanes.
+template <class T>
+__device__ __forceinline__ T* opaque(T* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 template <class M, int METHOD>
 __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma) {
   constexpr int S = M::S;
@@ -949,21 +959,23 @@ __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma
     return;
   }
 
-  double chi = Row(ma.cur, W).ld(off), rsq = Row(ma.cur + W, W).ld(off), aic = Row(ma.cur + 2 * W, W).ld(off);
-  double nacc = Row(ma.cur + 3 * W, W).ld(off);
-  int32_t status = ma.status ? ma.status[w] : 0;
+  // The current chain point (chi, R², AIC, acceptance count; status) also stays in
+  // HBM (cur rows): read after the proposal's integration, written on accept, so none
+  // of it holds registers across the integration.
+  double* __restrict__ cur = ma.cur;
   const int PS = P + 5;
 
   for (int it = ma.it0; it < ma.it1; ++it) {
     // ---- proposal: θ' = exp(log θ + N(0, sd)) for walking parameters (Framework.py:107-122)
     double tn[PMAX];
-    const double* dz = ma.dz + (int64_t)(it - ma.draw_it0) * P * W;
+    theta = opaque(theta);
+    y0g = opaque(y0g);
+    const double* dz = opaque(ma.dz + (int64_t)(it - ma.draw_it0) * P * W);
 #pragma unroll
     for (int j = 0; j < PMAX; ++j) {
       const double thj = (j < P) ? Row(theta + (int64_t)j * W, W).ld(off) : 0.0;
       tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? oe_exp(oe_log(thj) + Row(dz + (int64_t)j * W, W).ld(off)) : thj;
     }
-    const double u = Row(ma.u + (int64_t)(it - ma.draw_it0) * W, W).ld(off);
     // '<state>0' parameters drive initial states (Samplers.py:110-114)
     double y[S];
 #pragma unroll
@@ -975,6 +987,12 @@ __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma
     Acc a = acc_init();
     integrate_walker<M, PMAX, METHOD, false, false>(pb, y, tn, nullptr, W, w, active, a);
     const double chin = a.nvalid ? a.chi : __builtin_nan("");
+    theta = opaque(theta);
+    y0g = opaque(y0g);
+    cur = opaque(cur);
+    const double u = Row(opaque(ma.u + (int64_t)(it - ma.draw_it0) * W), W).ld(off);
+    double chi = Row(cur, W).ld(off), rsq = Row(cur + W, W).ld(off), aic = Row(cur + 2 * W, W).ld(off);
+    double nacc = Row(cur + 3 * W, W).ld(off);
     // ---- acceptance, in the reference's arithmetic (Samplers.py:124-127)
     const double lr = oe_exp(chi - chin);
     const double accp = oe_exp(oe_log(lr));
@@ -984,11 +1002,15 @@ __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma
       rsq = 1.0 - a.ssres / pb.sstot;
       aic = -2.0 * (-chi) + 2.0 * (double)pb.pnum;
       nacc += 1.0;
-      status = finish(a);
       if (active) {
 #pragma unroll
         for (int j = 0; j < PMAX; ++j)
           if (j < P) Row(theta + (int64_t)j * W, W).st(off, tn[j]);
+        Row(cur, W).st(off, chi);
+        Row(cur + W, W).st(off, rsq);
+        Row(cur + 2 * W, W).st(off, aic);
+        Row(cur + 3 * W, W).st(off, nacc);
+        if (ma.status) ma.status[w] = finish(a);
       }
     }
     // linked initial states follow the current parameters: the accepted proposal, or
@@ -1012,13 +1034,6 @@ __global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma
       Row(row + (int64_t)(P + 3) * W, W).st(off, (double)it);
       Row(row + (int64_t)(P + 4) * W, W).st(off, nacc / (double)it);
     }
-  }
-  if (active) {
-    Row(ma.cur, W).st(off, chi);
-    Row(ma.cur + W, W).st(off, rsq);
-    Row(ma.cur + 2 * W, W).st(off, aic);
-    Row(ma.cur + 3 * W, W).st(off, nacc);
-    if (ma.status) ma.status[w] = status;
   }
 }
 
