@@ -307,7 +307,8 @@ def _mh_inputs(spec, W, method="rk4", extra=None):
     return m, P, theta, y0
 
 
-@pytest.mark.parametrize("spec,method", [("one_i", "rk4"), ("two_i", "rk4"), ("two_i", "dopri5"), ("chain8", "rk4")])
+@pytest.mark.parametrize("spec,method", [("one_i", "rk4"), ("two_i", "rk4"), ("two_i", "dopri5"), ("chain8", "rk4"),
+                                         ("chain20", "rk4"), ("chain20", "dopri5")])
 def test_mh_philox_vs_c_restatement(spec, method):
     m, P, theta, y0 = _mh_inputs(spec, 130, method)
     walk = np.ones(P, np.uint8)
