@@ -1,0 +1,88 @@
+"""Register / scratch budgets of the hot kernels, read from the compiler (CPU, no GPU).
+
+A kernel that starts spilling is still bitwise correct, so parity tests do not see it;
+the chain20 DOPRI5 MH kernel once doubled in time (13.4 vs 6.3 ms per iteration,
+DESIGN.md §3.4 r01k) after unrelated integrator changes pushed it to 432 B/lane of
+scratch.  These budgets catch that at build time: hipcc's kernel-resource-usage remarks
+for the two translation units the bench and the C3 configs use.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "odelib_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950",
+         "-Rpass-analysis=kernel-resource-usage", "-c", "-o", os.devnull]
+
+_FIELDS = {"VGPRs": "vgpr", "AGPRs": "agpr", "ScratchSize [bytes/lane]": "scratch",
+           "Occupancy [waves/SIMD]": "occupancy", "SGPRs Spill": "sgpr_spill", "VGPRs Spill": "vgpr_spill"}
+
+
+def _parse(text):
+    kernels, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = kernels.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([^:]+): (\d+)", line)
+        if m and cur is not None and m.group(1).strip() in _FIELDS:
+            cur[_FIELDS[m.group(1).strip()]] = int(m.group(2))
+    return kernels
+
+
+@pytest.fixture(scope="module")
+def resources():
+    if not os.path.exists(HIPCC) and shutil.which("hipcc") is None:
+        pytest.skip("hipcc not available")
+    units = ["inst_two_i.hip", "inst_chain20.hip"]
+    procs = {u: subprocess.Popen([HIPCC, *FLAGS, u], cwd=CSRC, stdout=subprocess.PIPE,
+                                 stderr=subprocess.STDOUT, text=True) for u in units}
+    out = {}
+    for u, p in procs.items():
+        text, _ = p.communicate(timeout=600)
+        assert p.returncode == 0, text[-2000:]
+        out[u] = _parse(text)
+    return out
+
+
+def _find(kernels, *needles):
+    hits = [v for k, v in kernels.items() if all(n in k for n in needles)]
+    assert len(hits) == 1, (needles, list(kernels))
+    return hits[0]
+
+
+# mangled-name fragments: k_integrate<M, METHOD(0 RK4, 1 DOPRI5), TRAJ, NT>, k_mh<M, METHOD>
+C1 = ("k_integrateINS_4TwoIELi0ELb1ELb1E",)
+C2 = ("k_integrateINS_4TwoIELi1ELb1ELb1E",)
+C3 = ("k_integrateINS_5ChainILi20EEELi0ELb1ELb1E",)
+MH_TWO_I_RK4 = ("k_mhINS_4TwoIELi0E",)
+MH_TWO_I_DOPRI5 = ("k_mhINS_4TwoIELi1E",)
+MH_CHAIN20_RK4 = ("k_mhINS_5ChainILi20EEELi0E",)
+MH_CHAIN20_DOPRI5 = ("k_mhINS_5ChainILi20EEELi1E",)
+
+
+def test_two_i_kernels_never_spill(resources):
+    for name, r in resources["inst_two_i.hip"].items():
+        assert r["scratch"] == 0 and r["vgpr_spill"] == 0, (name, r)
+
+
+@pytest.mark.parametrize("needles,min_occ", [(C1, 4), (C2, 2), (MH_TWO_I_RK4, 4), (MH_TWO_I_DOPRI5, 2)])
+def test_two_i_occupancy(resources, needles, min_occ):
+    r = _find(resources["inst_two_i.hip"], *needles)
+    assert r["occupancy"] >= min_occ, r
+
+
+def test_chain20_rk4_kernels_fit_registers(resources):
+    for needles in (C3, MH_CHAIN20_RK4):
+        r = _find(resources["inst_chain20.hip"], *needles)
+        assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and r["occupancy"] >= 2, (needles, r)
+
+
+def test_chain20_dopri5_mh_scratch_budget(resources):
+    r = _find(resources["inst_chain20.hip"], *MH_CHAIN20_DOPRI5)
+    assert r["scratch"] <= 192, r  # 160 B/lane at r01k; 432 when it ran 2x slower
