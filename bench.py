@@ -224,7 +224,9 @@ def main():
             dist.init_process_group(backend)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
 
+    m.device = dev_index  # this rank's GPU (the model's default device is 0)
     eng = m.engine()
+    assert eng.device == dev_index
     fp = eng.problem
     S, T = fp.n_states, fp.n_times
     Wl = args.walkers
@@ -340,6 +342,7 @@ def main():
                                        ("C3-dopri5", "chain20", "dopri5", 262144),
                                        ("C4-shard", "two_i", "rk4", 131072)):
             mx, y0x = build_problem(model, method, T)
+            mx.device = dev_index
             ex = mx.engine()
             Sx = len(y0x)
             thx = torch.as_tensor(synthetic_walkers(W, P), device=dev).contiguous()
