@@ -8,7 +8,8 @@ ODE callable is bound to a compiled device RHS by ``models.resolve``.
 
 Engine options (keyword-only, new): ``method`` ('dopri5' default — adaptive like
 odeint — or 'rk4'), ``rtol``/``atol`` (odeint defaults), ``rk4_substeps``,
-``max_steps`` (odeint's mxstep), ``device`` (HIP device index), ``device_model``
+``max_steps`` (odeint's mxstep), ``device`` (HIP device index; default: torch's current
+device when the engine is built), ``device_model``
 (force a built-in RHS, or 'rtc'), ``device_rhs`` (C++ body of the RHS for hipRTC).
 An ODE callable that matches no built-in is transpiled to C and compiled at run time.
 ``MCMC`` runs every chain as one walker of a single batched launch; ``rng='replay'``
@@ -119,7 +120,9 @@ class ModelFramework:
         self.atol = float(eng.get("atol", ODEINT_TOL))
         self.rk4_substeps = int(eng.get("rk4_substeps", 1))
         self.max_steps = int(eng.get("max_steps", 500))
-        self.device = int(eng.get("device", 0))
+        # None: torch's current device when the engine is built (under torchrun, the GPU
+        # the rank selected with torch.cuda.set_device), as torch's own default is
+        self.device = None if eng.get("device") is None else int(eng["device"])
         self.device_model = eng.get("device_model", None)
         self.device_rhs = eng.get("device_rhs", None)
         self._engine = None
@@ -363,12 +366,16 @@ class ModelFramework:
                           max_steps=self.max_steps, custom_source=dm.source)
 
     def engine(self) -> Engine:
-        key = (self.method, self.rtol, self.atol, self.rk4_substeps, self.max_steps, self.device,
+        device = self.device
+        if device is None:
+            import torch
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        key = (self.method, self.rtol, self.atol, self.rk4_substeps, self.max_steps, device,
                self.device_model, self.device_rhs, id(self.df), len(self.times), float(self.times[-1]))
         if self._engine is None or self._engine_key != key:
             fp = self.fit_problem()
-            if self._engine is None or self._engine.device != self.device:
-                self._engine = Engine(fp, device=self.device)
+            if self._engine is None or self._engine.device != device:
+                self._engine = Engine(fp, device=device)
             else:
                 self._engine.set_problem(fp)
             self._engine_key = key
