@@ -251,3 +251,25 @@ def test_checkpoint_roundtrip(tmp_path):
     for k in ("theta", "y0", "final", "status"):
         assert np.array_equal(back[k], res[k])
     assert back["next_it"] == 12 and back["meta"] == {"seed": 3}
+
+
+def test_engine_binds_torch_current_device(monkeypatch):
+    """Without device=, the engine is built on torch's current device (the rank's GPU
+    under torchrun after torch.cuda.set_device), not on GPU 0; device= overrides it."""
+    import torch
+    import odelib_amd.Framework as F
+
+    class FakeEngine:
+        def __init__(self, fp, device=0):
+            self.device = device
+
+        def set_problem(self, fp):
+            pass
+
+    monkeypatch.setattr(F, "Engine", FakeEngine)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    m = product_model("two_i")
+    assert m.engine().device == 3
+    m.device = 1
+    assert m.engine().device == 1
