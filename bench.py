@@ -319,6 +319,7 @@ def main():
         # Fitting-report statistics of the pooled posterior (rawstats, Framework.py:11-17)
         # from two all-reduces of per-parameter sufficient statistics
         from odelib_amd.distributed import pooled_rawstats
+        pooled_rawstats(r["samples"], P)  # untimed: first use loads torch's reduction kernels
         torch.cuda.synchronize(dev)
         tr0 = time.perf_counter()
         med, _ = pooled_rawstats(r["samples"], P)
