@@ -904,7 +904,10 @@ struct MHArgs {
 struct Row {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ Row(const double* row, int64_t W)
-      : r(__builtin_amdgcn_make_buffer_rsrc((void*)row, 0, (int)(W * 8), 0x00020000)) {}
+      // num_records is 32 bits: W = 2^29 (the ABI maximum) makes W*8 = 2^32, clamp it
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)row, 0,
+                                            (int)(uint32_t)(W * 8 > 0xffffffffll ? 0xffffffffll : W * 8),
+                                            0x00020000)) {}
   __device__ __forceinline__ double ld(uint32_t off) const {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
   }
