@@ -18,6 +18,7 @@ on device for large ensembles.
 """
 from __future__ import annotations
 
+import itertools
 import random as rd
 import warnings
 
@@ -30,6 +31,9 @@ from .engine import ODEINT_TOL, Engine, FitProblem
 from .rng import legacy_replay_streams
 
 _ENGINE_KW = ("method", "rtol", "atol", "rk4_substeps", "max_steps", "device", "device_model", "device_rhs")
+# One token per distinct data set-up (constructor / reset_dataframe).  copy() keeps the
+# token because the copy's observations are equal to the original's.
+_DATA_TOKENS = itertools.count()
 
 
 def rawstats(pdseries):
@@ -126,7 +130,7 @@ class ModelFramework:
         self.device_model = eng.get("device_model", None)
         self.device_rhs = eng.get("device_rhs", None)
         self._engine = None
-        self._engine_key = None
+        self._data_token = next(_DATA_TOKENS)
 
         self.parameters = {el: None for el in self._pnames}
         self.istates = {el: 0 for el in self._snames}  # Framework.py:216
@@ -179,7 +183,7 @@ class ModelFramework:
             if org not in _is:
                 _is[org] = abundance
         self.set_inits(**_is)
-        self._engine_key = None
+        self._data_token = next(_DATA_TOKENS)
 
     def _formatdf(self, df):
         """normalise the two accepted dataframe layouts (Framework.py:281-307)"""
@@ -338,7 +342,7 @@ class ModelFramework:
     def fit_problem(self) -> FitProblem:
         """Constant kernel inputs."""
         dm = _models.resolve_model(self._model, len(self._snames), len(self._pnames), self.device_model,
-                                   self.device_rhs)
+                                   self.device_rhs, times=self.times)
         mid, S = (dm.model_id if dm.model_id is not None else -1), dm.n_states
         _, cols, keep = self._obs_layout()
         tidx, mask, O, Ssig, lin = [], [], [], [], []
@@ -365,21 +369,29 @@ class ModelFramework:
                           rk4_substeps=self.rk4_substeps, rtol=self.rtol, atol=self.atol,
                           max_steps=self.max_steps, custom_source=dm.source)
 
+    def _problem_key(self, device):
+        """What the uploaded FitProblem depends on.  It is recorded on the Engine itself
+        (``Engine.key``): copies share one Engine, and a copy with other data re-uploads
+        its problem, after which the original's next ``engine()`` sees a foreign key and
+        uploads its own again."""
+        return (self.method, self.rtol, self.atol, self.rk4_substeps, self.max_steps, device,
+                self.device_model, self.device_rhs, self._data_token, int(self._pnum),
+                len(self.times), float(self.times[0]), float(self.times[-1]))
+
     def engine(self) -> Engine:
         device = self.device
         if device is None:
             import torch
             device = torch.cuda.current_device() if torch.cuda.is_available() else 0
-        key = (self.method, self.rtol, self.atol, self.rk4_substeps, self.max_steps, device,
-               self.device_model, self.device_rhs, id(self.df), len(self.times), float(self.times[-1]))
-        if self._engine is None or self._engine_key != key:
-            fp = self.fit_problem()
-            if self._engine is None or self._engine.device != device:
-                self._engine = Engine(fp, device=device)
-            else:
-                self._engine.set_problem(fp)
-            self._engine_key = key
-        return self._engine
+        key = self._problem_key(device)
+        eng = self._engine
+        if eng is None or eng.device != device:
+            eng = Engine(self.fit_problem(), device=device)
+            eng.key = key
+            self._engine = eng
+        elif getattr(eng, "key", None) != key:
+            eng.set_problem(self.fit_problem(), key=key)
+        return eng
 
     def _theta_matrix(self, rows):
         """list of parameter vectors -> [P][W] float64"""
@@ -520,7 +532,7 @@ class ModelFramework:
     def copy(self, overwrite=dict()):
         newmod = ModelFramework.__new__(ModelFramework)
         for attr, v in self.__dict__.items():
-            if attr in ('parameters', '_engine', '_engine_key'):
+            if attr in ('parameters', '_engine'):
                 continue
             if isinstance(v, (list, dict, pd.DataFrame, np.ndarray)):
                 newmod.__dict__[attr] = v.copy()
@@ -528,8 +540,7 @@ class ModelFramework:
                 newmod.__dict__[attr] = v
         newmod.parameters = {p: (self.parameters[p].copy() if self.parameters[p] is not None else None)
                              for p in self.parameters}
-        newmod._engine = self._engine  # contexts are reusable across copies of one problem
-        newmod._engine_key = self._engine_key
+        newmod._engine = self._engine  # shared context; engine() checks Engine.key before use
         _ps = {el: overwrite[el] for el in overwrite if el in newmod._pnames}
         _is = {el: overwrite[el] for el in overwrite if el in newmod._snames}
         if _ps:

@@ -161,10 +161,28 @@ int ensure_np_state(oe_ctx* c, int64_t W, NpState* st) {
   return OE_OK;
 }
 
-int set_device(oe_ctx* c) {
-  OE_HIP(c, hipSetDevice(c->device));
-  return OE_OK;
-}
+// Switches the calling thread to the context's device for one ABI call and restores the
+// caller's device on return: torch (and any other HIP user in the process) reads the same
+// thread-current device, so an Engine on device k must not move torch's default device.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != device) err = hipSetDevice(device);
+    else prev = -1;  // already current: nothing to restore
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
+#define OE_DEVICE_GUARD(ctx)                                                              \
+  DeviceGuard device_guard_((ctx)->device);                                               \
+  if (device_guard_.err != hipSuccess)                                                    \
+    return fail(ctx, OE_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(device_guard_.err))
 
 }  // namespace
 
@@ -212,7 +230,8 @@ int oe_ctx_create(int32_t device, oe_ctx** out) {
     *out = c;
     return OE_ERR_HIP;
   }
-  if (hipSetDevice(device) != hipSuccess ||
+  DeviceGuard dg(device);
+  if (dg.err != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     c->err = "oe_ctx_create: HIP initialisation failed";
@@ -234,7 +253,7 @@ int oe_ctx_create(int32_t device, oe_ctx** out) {
 void oe_ctx_destroy(oe_ctx* c) {
   if (!c) return;
   if (c->own_stream) {
-    (void)hipSetDevice(c->device);
+    DeviceGuard dg(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->d_times) (void)hipFree(c->d_times);
     if (c->d_obs) (void)hipFree(c->d_obs);
@@ -277,8 +296,7 @@ int oe_model_compile(oe_ctx* c, const char* rhs_body, int32_t n_states, int32_t 
       return OE_OK;
     }
   }
-  int rc = set_device(c);
-  if (rc) return rc;
+  OE_DEVICE_GUARD(c);
   auto m = std::make_unique<CustomModel>();
   std::string err;
   if (rtc_build(rhs_body, n_states, n_params, c->arch.c_str(), &m->rtc, err)) return fail(c, OE_ERR_ARG, err);
@@ -307,8 +325,7 @@ int oe_ctx_use_own_stream(oe_ctx* c) {
 int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   if (!c || !c->own_stream) return OE_ERR_STATE;
   if (!p) return fail(c, OE_ERR_ARG, "oe_problem_set: null problem");
-  int rc = set_device(c);
-  if (rc) return rc;
+  OE_DEVICE_GUARD(c);
   const Entry* e = nullptr;
   if (p->model_id >= OE_MODEL_CUSTOM) {
     const size_t k = (size_t)(p->model_id - OE_MODEL_CUSTOM);
@@ -408,8 +425,8 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   if (!c->has_problem) return fail(c, OE_ERR_STATE, "oe_integrate: call oe_problem_set first");
   if (W <= 0 || W > kMaxWalkers) return fail(c, OE_ERR_ARG, "oe_integrate: n_walkers must be in [1, 2^29]");
   if (!y0 || !theta) return fail(c, OE_ERR_ARG, "oe_integrate: y0 and theta are required");
-  int rc = set_device(c);
-  if (rc) return rc;
+  OE_DEVICE_GUARD(c);
+  int rc = OE_OK;
   const Entry* e = c->entry;
   const int S = e->S, P = c->dp.P, T = c->dp.T;
   const bool host = flags & OE_HOST_PTRS;
@@ -516,8 +533,8 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
     return fail(c, OE_ERR_ARG, "oe_mh_run: unknown rng_mode");
   }
   if (S > 64) return fail(c, OE_ERR_UNSUPPORTED, "oe_mh_run: S > 64");
-  int rc = set_device(c);
-  if (rc) return rc;
+  OE_DEVICE_GUARD(c);
+  int rc = OE_OK;
 
   MHArgs m{};
   m.W = W;
@@ -638,8 +655,8 @@ int oe_numpy_streams(oe_ctx* c, int64_t W, const uint32_t* seeds, int32_t nits, 
     return fail(c, OE_ERR_ARG, "oe_numpy_streams: need nits >= 1, 1 <= n_params <= 64, prior_draws >= 0");
   if (!seeds || !walk_mask || (nits > 1 && (!dz || !u)))
     return fail(c, OE_ERR_ARG, "oe_numpy_streams: seeds, walk_mask, dz and u are required");
-  int rc = set_device(c);
-  if (rc) return rc;
+  OE_DEVICE_GUARD(c);
+  int rc = OE_OK;
   if (nits == 1) return OE_OK;
   NpDrawArgs nd{};
   nd.W = W;

@@ -96,6 +96,70 @@ def _torch():
     return torch
 
 
+def _row_digest(a, k: int) -> str:
+    """blake2b of row ``k`` of a replay stream (numpy array or tensor on any device)."""
+    import hashlib
+    r = a[k]
+    r = r.detach().cpu().numpy() if hasattr(r, "detach") else np.asarray(r)
+    return hashlib.blake2b(np.ascontiguousarray(r, dtype=np.float64).tobytes(), digest_size=16).hexdigest()
+
+
+def rng_record(rng, seed, walker_offset, step_sd, walk_mask, burnin, prior_draws=0, replay=None, nits=0):
+    """What a chain's random draws depend on, saved with a checkpoint (``checkpoint.save``)
+    and checked when the chains are resumed (``check_resume``).  Replay streams are
+    identified by digests of their first and last used rows."""
+    rec = {"rng": str(rng), "seed": int(seed) & 0xFFFFFFFFFFFFFFFF, "walker_offset": int(walker_offset),
+           "step_sd": float(step_sd), "walk_mask": [int(v) for v in np.asarray(walk_mask).reshape(-1)],
+           "burnin": int(burnin), "prior_draws": int(prior_draws) if rng == "numpy" else 0}
+    n = int(nits) - 1
+    if rng == "replay" and replay is not None and n > 0:
+        rec["replay_rows"] = [0, n - 1]
+        rec["replay_digest"] = [_row_digest(replay[0], 0), _row_digest(replay[1], 0),
+                                _row_digest(replay[0], n - 1), _row_digest(replay[1], n - 1)]
+    return rec
+
+
+def check_resume(resume, rec, numpy_seeds=None):
+    """Raise ValueError unless resuming ``resume`` with the draws described by ``rec``
+    (``rng_record`` of the resuming call) continues the checkpointed chains exactly as
+    one uninterrupted run would.  Returns the numpy seeds to use (the call's, else the
+    checkpoint's)."""
+    old = resume.get("rng_state")
+    if old is None:
+        raise ValueError("the checkpoint records no random-stream state (written by an older version); "
+                         "cannot verify that resuming reproduces one uninterrupted run")
+    for k in ("rng", "step_sd", "walk_mask", "burnin"):
+        if old.get(k) != rec.get(k):
+            raise ValueError(f"resume: {k}={rec.get(k)!r} differs from the checkpoint's {old.get(k)!r}")
+    if rec["rng"] == "philox":
+        for k in ("seed", "walker_offset"):
+            if old[k] != rec[k]:
+                raise ValueError(f"resume: philox {k}={rec[k]} differs from the checkpoint's {old[k]}")
+    saved_seeds = resume.get("numpy_seeds")
+    if rec["rng"] == "numpy":
+        if old["prior_draws"] != rec["prior_draws"]:
+            raise ValueError(f"resume: prior_draws={rec['prior_draws']} differs from the checkpoint's "
+                             f"{old['prior_draws']}")
+        if numpy_seeds is None:
+            numpy_seeds = saved_seeds
+        elif saved_seeds is not None and not np.array_equal(np.asarray(numpy_seeds, np.int64),
+                                                            np.asarray(saved_seeds, np.int64)):
+            raise ValueError("resume: numpy_seeds differ from the checkpoint's")
+    if rec["rng"] == "replay" and "replay_digest" in old:
+        if "replay_digest" not in rec:
+            raise ValueError("resume: rng='replay' needs the replay streams")
+        # rows the checkpointed run consumed must be the same rows in the resuming streams
+        first, last = old["replay_rows"]
+        if rec.get("_replay") is not None:
+            dz, u = rec["_replay"]
+            if len(dz) <= last or len(u) <= last:
+                raise ValueError("resume: replay streams are shorter than the checkpointed run")
+            got = [_row_digest(dz, first), _row_digest(u, first), _row_digest(dz, last), _row_digest(u, last)]
+            if got != old["replay_digest"]:
+                raise ValueError("resume: replay streams differ from the ones the checkpointed run used")
+    return numpy_seeds
+
+
 def _ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
 
@@ -113,16 +177,21 @@ class Engine:
         self.ctx = N.Context(self.device)
         self.use_torch_stream = use_torch_stream
         self.problem = None
+        self.key = None
         self.set_problem(problem)
 
     # -- problem ---------------------------------------------------------------------------
-    def set_problem(self, problem: FitProblem):
+    def set_problem(self, problem: FitProblem, key=None):
+        """Upload ``problem``; ``key`` is an owner's label for it (``ModelFramework``
+        compares it before reusing a shared engine) and is cleared by an unlabelled upload."""
+        self.key = None
         self._sync_stream()
         c = problem.to_c()
         if problem.custom_source is not None:  # compiled once per context (cached by source)
             c.model_id = self.ctx.model_compile(problem.custom_source, problem.n_states, problem.n_params)
         self.ctx.problem_set(c)
         self.problem = problem
+        self.key = key
 
     def _sync_stream(self):
         if self.use_torch_stream:
@@ -226,7 +295,10 @@ class Engine:
         nits = int(nits)
         burnin = int(burnin)
         it_start = 1
+        rec = rng_record(rng, seed, walker_offset, step_sd, walk_mask, burnin, prior_draws, replay, nits)
         if resume is not None:
+            chk = dict(rec, _replay=replay if rng == "replay" else None)
+            numpy_seeds = check_resume(resume, chk, numpy_seeds)
             it_start = int(resume["next_it"])
             theta, y0 = resume["theta"], resume["y0"]
         W = int((theta if isinstance(theta, torch.Tensor) else np.asarray(theta)).shape[1])
@@ -291,8 +363,11 @@ class Engine:
         self.ctx.mh_run(a, N.OE_ASYNC)
         if sync:
             torch.cuda.synchronize(self.dev)
-        return {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status,
-                "next_it": max(nits, it_start), "_keep": keep}
+        out = {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status,
+               "next_it": max(nits, it_start), "rng_state": rec, "_keep": keep}
+        if rng == "numpy":
+            out["numpy_seeds"] = np.asarray(numpy_seeds, dtype=np.int64)
+        return out
 
     def close(self):
         self.ctx.close()

@@ -2,20 +2,20 @@
 ``__device__`` RHS (odelib_amd/csrc/models.cuh).
 
 The reference passes the Python callable straight to odeint (ODElib/Framework.py:656).
-The engine cannot run Python on the GPU, so ``resolve`` finds the compiled RHS that
-computes the same function: either the one named by ``device_model=``, or — by
-default — the built-in whose output agrees with the user's callable on a set of
-random positive probe points.  The probe is host-side validation only; no result
-of the fit ever comes from the Python callable.
+The engine cannot run Python on the GPU, so ``resolve_model`` finds the device RHS that
+computes the same function: the one named by ``device_model=``, a built-in whose exact
+algebraic form equals the transpiled callable's, or the callable itself transpiled to C
+and compiled with hipRTC.  No result of the fit ever comes from the Python callable.
 """
 from __future__ import annotations
 
+import warnings
 from dataclasses import dataclass
 
 import numpy as np
 
 from . import _native as N
-from .transpile import Unsupported, transpile
+from .transpile import Unsupported, polynomial_form, transpile
 
 
 @dataclass
@@ -88,12 +88,19 @@ def candidates(n_states: int, n_params: int):
     return out
 
 
-def _probe_equal(user, ref, n_states, n_params, trials=8, rtol=1e-12):
+def _probe_equal(user, ref, n_states, n_params, trials=8, rtol=1e-12, times=None):
+    """Numerical agreement on random positive states/parameters, with t drawn from the
+    problem's whole time grid (both ends included) when ``times`` is given."""
     rng = np.random.default_rng(12345)
-    for _ in range(trials):
+    if times is not None and len(times):
+        tv = np.asarray(times, float)
+        t_probe = np.r_[tv[0], tv[-1], rng.choice(tv, size=max(trials - 2, 0))]
+    else:
+        t_probe = rng.uniform(0, 3, trials)
+    for k in range(len(t_probe)):
         y = rng.uniform(0.5, 2.0, n_states) * 10.0 ** rng.uniform(-2, 7, n_states)
         ps = list(rng.uniform(0.5, 2.0, n_params) * 10.0 ** rng.uniform(-8, 1, n_params))
-        t = float(rng.uniform(0, 3))
+        t = float(t_probe[k])
         try:
             a = np.asarray(user(y, t, ps), dtype=float).reshape(-1)
         except Exception:
@@ -104,49 +111,78 @@ def _probe_equal(user, ref, n_states, n_params, trials=8, rtol=1e-12):
     return True
 
 
-def resolve(ode, n_states: int, n_params: int, device_model: str | None = None):
+def _builtin_form(f, n_states, n_params):
+    return polynomial_form(transpile(f, n_states, n_params))
+
+
+def resolve(ode, n_states: int, n_params: int, device_model: str | None = None, times=None):
     """Return (model_id, n_states) of the compiled built-in RHS equal to ``ode``."""
-    dm = resolve_model(ode, n_states, n_params, device_model, allow_rtc=False)
+    dm = resolve_model(ode, n_states, n_params, device_model, allow_rtc=False, times=times)
     return dm.model_id, dm.n_states
 
 
 def resolve_model(ode, n_states: int, n_params: int, device_model: str | None = None,
-                  device_rhs: str | None = None, allow_rtc: bool = True) -> DeviceModel:
+                  device_rhs: str | None = None, allow_rtc: bool = True, times=None) -> DeviceModel:
     """Choose the device RHS for ``ode``:
 
     1. ``device_rhs`` (C++ body of ``rhs(y, t, ps, dy)``)  -> hipRTC, as given;
     2. ``device_model`` naming a built-in ('zero_i', 'one_i', 'two_i', 'chain') -> that
-       built-in, after checking the callable computes the same function;
-       ``device_model='rtc'`` forces the transpiled path;
-    3. otherwise the first built-in that agrees with the callable on probe points;
+       built-in, after checking the callable computes the same function: exactly (the
+       algebraic form below) when the callable transpiles, otherwise numerically on
+       probe points over the time grid, with a warning; ``device_model='rtc'`` forces
+       the transpiled path;
+    3. otherwise a built-in only when the callable is PROVABLY the same function: it
+       transpiles, it is a polynomial in y and ps (no t, no calls, no branches) and its
+       exact normal form (``transpile.polynomial_form``: expanded monomials with rational
+       coefficients) equals the built-in's.  Agreement on probe points alone never
+       binds a callable: a term switched on by t or by the state outside the probed
+       region would otherwise be silently replaced;
     4. otherwise the callable transpiled to C (``transpile.py``), checked against the
-       callable on probe points, compiled with hipRTC."""
+       callable on probe points over the time grid, compiled with hipRTC.
+    ``times`` is the problem's output grid (probe times)."""
     if device_rhs is not None:
         return DeviceModel("custom-source", n_states, source=device_rhs)
     cands = candidates(n_states, n_params)
+    tr, why = None, None
+    if ode is not None:
+        try:
+            tr = transpile(ode, n_states, n_params)
+        except Unsupported as exc:
+            why = exc
     if device_model is not None and device_model != "rtc":
         cands = [c for c in cands if c[0] == device_model]
         if not cands:
             raise ValueError(f"device_model={device_model!r} has no compiled RHS with S={n_states}, "
                              f"P={n_params}")
         name, mid, S, P, f = cands[0]
-        if ode is not None and not _probe_equal(ode, f, n_states, n_params):
-            raise ValueError(f"the ODE callable does not match the compiled {name!r} right-hand side")
+        if ode is not None:
+            if tr is not None:  # exact: same normal form, or it is not this built-in
+                form = polynomial_form(tr)
+                if form is None or form != _builtin_form(f, n_states, n_params):
+                    raise ValueError(f"the ODE callable is not algebraically the compiled {name!r} right-hand "
+                                     "side (it differs, or reads t / branches / calls a function); omit "
+                                     "device_model to run it through hipRTC")
+            elif not _probe_equal(ode, f, n_states, n_params, times=times):
+                raise ValueError(f"the ODE callable does not match the compiled {name!r} right-hand side")
+            else:
+                warnings.warn(f"device_model={name!r}: the ODE callable does not transpile, so it was checked "
+                              "against the compiled right-hand side numerically only (probe points over the "
+                              "time grid); the fit uses the compiled built-in", stacklevel=3)
         return DeviceModel(name, S, model_id=mid)
-    if device_model is None:
-        for name, mid, S, P, f in cands:
-            if ode is not None and _probe_equal(ode, f, n_states, n_params):
-                return DeviceModel(name, S, model_id=mid)
+    if device_model is None and tr is not None:
+        form = polynomial_form(tr)
+        if form is not None:
+            for name, mid, S, P, f in cands:
+                if form == _builtin_form(f, n_states, n_params):
+                    return DeviceModel(name, S, model_id=mid)
     if not allow_rtc or ode is None:
         raise NotImplementedError(
-            "no compiled device RHS matches this ODE callable; built-ins are "
+            "no compiled device RHS is provably equal to this ODE callable; built-ins are "
             f"{sorted(BUILTIN)} and chain<N> for N in {CHAIN_SIZES} (pass device_model=... or device_rhs=...)")
-    try:
-        tr = transpile(ode, n_states, n_params)
-    except Unsupported as exc:
+    if tr is None:
         raise NotImplementedError(
-            f"the ODE callable matches no built-in RHS and cannot be transpiled ({exc}); pass its C body as "
-            "device_rhs='...' (see include/odelib_amd.h oe_model_compile)") from exc
-    if not _probe_equal(ode, tr.evaluate, n_states, n_params):
+            f"the ODE callable cannot be transpiled ({why}); pass its C body as device_rhs='...' (see "
+            "include/odelib_amd.h oe_model_compile), or device_model='<built-in>' to assert that it is one")
+    if not _probe_equal(ode, tr.evaluate, n_states, n_params, times=times):
         raise NotImplementedError("the transpiled RHS does not reproduce the callable; pass device_rhs='...'")
     return DeviceModel("rtc:" + getattr(ode, "__name__", "ode"), n_states, source=tr.c_body)

@@ -740,6 +740,101 @@ def _c(e) -> str:
     raise AssertionError(k)
 
 
+_POLY_MAX_TERMS = 4096
+
+
+def _padd(a, b, sign=1):
+    out = dict(a)
+    for m, c in b.items():
+        v = out.get(m, 0) + sign * c
+        if v:
+            out[m] = v
+        else:
+            out.pop(m, None)
+    return out
+
+
+def _pmul(a, b):
+    out = {}
+    for ma, ca in a.items():
+        for mb, cb in b.items():
+            exps = dict(ma)
+            for v, e in mb:
+                exps[v] = exps.get(v, 0) + e
+            m = tuple(sorted(exps.items()))
+            c = out.get(m, 0) + ca * cb
+            if c:
+                out[m] = c
+            else:
+                out.pop(m, None)
+    if len(out) > _POLY_MAX_TERMS:
+        raise _NotPolynomial
+    return out
+
+
+class _NotPolynomial(Exception):
+    pass
+
+
+def _poly(e, env):
+    """Expression -> {monomial: exact rational coefficient}; monomial = sorted
+    ((('y'|'p'), index), exponent) pairs.  Raises _NotPolynomial for t, calls, branches,
+    comparisons and division by anything but a non-zero constant."""
+    from fractions import Fraction
+    k = e[0]
+    if k == "const":
+        c = Fraction(float(e[1]))
+        return {(): c} if c else {}
+    if k in ("y", "ps"):
+        return {((("y" if k == "y" else "p", e[1]), 1),): Fraction(1)}
+    if k == "var":
+        return env[e[1]]
+    if k == "neg":
+        return {m: -c for m, c in _poly(e[1], env).items()}
+    if k == "bin":
+        op = e[1]
+        a = _poly(e[2], env)
+        if op == "sq":
+            return _pmul(a, a)
+        b = _poly(e[3], env)
+        if op == "+":
+            return _padd(a, b)
+        if op == "-":
+            return _padd(a, b, -1)
+        if op == "*":
+            return _pmul(a, b)
+        if op == "/":
+            if set(b) != {()}:
+                raise _NotPolynomial
+            return {m: c / b[()] for m, c in a.items()}
+        if op == "pow":
+            if set(b) - {()}:
+                raise _NotPolynomial
+            n = b.get((), 0)
+            if n.denominator != 1 or not 0 <= n <= 8:
+                raise _NotPolynomial
+            out = {(): Fraction(1)}
+            for _ in range(int(n)):
+                out = _pmul(out, a)
+            return out
+    raise _NotPolynomial
+
+
+def polynomial_form(tr: "TranspiledRHS"):
+    """Exact algebraic normal form of a transpiled RHS: one {monomial: rational
+    coefficient} per dy[k], or None when the RHS is not a polynomial in y and ps with
+    constant coefficients (it reads t, calls a function, branches on data, or divides by
+    a non-constant).  Two right-hand sides with equal forms compute the same
+    mathematical function; they can differ only in floating-point rounding order."""
+    env = {}
+    try:
+        for name, expr in tr._stmts:
+            env[name] = _poly(expr, env)
+        return tuple(tuple(sorted(_poly(e, env).items())) for e in tr._outs)
+    except _NotPolynomial:
+        return None
+
+
 def transpile(func, n_states: int, n_params: int) -> TranspiledRHS:
     tr = _Translator(func, n_states, n_params)
     tr.run()

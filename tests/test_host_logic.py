@@ -262,9 +262,10 @@ def test_engine_binds_torch_current_device(monkeypatch):
     class FakeEngine:
         def __init__(self, fp, device=0):
             self.device = device
+            self.key = None
 
-        def set_problem(self, fp):
-            pass
+        def set_problem(self, fp, key=None):
+            self.key = key
 
     monkeypatch.setattr(F, "Engine", FakeEngine)
     monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
@@ -273,3 +274,163 @@ def test_engine_binds_torch_current_device(monkeypatch):
     assert m.engine().device == 3
     m.device = 1
     assert m.engine().device == 1
+
+
+class _RecordingEngine:
+    """Engine stand-in recording the uploaded FitProblem (no GPU)."""
+    uploads = 0
+
+    def __init__(self, fp, device=0):
+        self.device = device
+        self.key = None
+        self.problem = fp
+        _RecordingEngine.uploads += 1
+
+    def set_problem(self, fp, key=None):
+        self.problem = fp
+        self.key = key
+        _RecordingEngine.uploads += 1
+
+
+def test_copy_with_other_data_does_not_leak_into_original(monkeypatch):
+    """copies share one Engine; a copy that resets its dataframe must not
+    leave the original integrating on the copy's grid / scoring the copy's data."""
+    import odelib_amd.Framework as F
+    from helpers import CONFIGS, demo_df
+    monkeypatch.setattr(F, "Engine", _RecordingEngine)
+    m = product_model("two_i", device=0)
+    e0 = m.engine()
+    t_orig, obs_orig = e0.problem.times.copy(), e0.problem.obs_log.copy()
+    m2 = m.copy()
+    assert m2.engine() is e0 and e0.problem.times[-1] == t_orig[-1]  # same data: no re-upload needed
+    n_up = _RecordingEngine.uploads
+    df2 = demo_df(CONFIGS["two_i"]["rename"])
+    df2["time"] = df2["time"] * 2.0
+    df2["abundance"] = df2["abundance"] * 3.0
+    m2.reset_dataframe(df2)
+    assert m2.engine().problem.times[-1] == 2.0 * t_orig[-1]
+    # the original re-uploads its own problem before its next use
+    p = m.engine().problem
+    assert np.array_equal(p.times, t_orig) and np.array_equal(p.obs_log, obs_orig)
+    assert np.array_equal(m.times, t_orig)
+    assert _RecordingEngine.uploads == n_up + 2
+    # and the copy again
+    assert m2.engine().problem.times[-1] == 2.0 * t_orig[-1]
+    # an unchanged model reuses the upload
+    n_up = _RecordingEngine.uploads
+    m2.engine()
+    assert _RecordingEngine.uploads == n_up
+
+
+def test_checkpoint_records_rng_state_and_resume_checks_it(tmp_path):
+    """a checkpoint carries what the chains' draws depend on, and a resume
+    with other draws (rng mode, Philox seed / walker offset, numpy seeds, prior draws,
+    replay streams) is refused instead of silently producing a different chain."""
+    from odelib_amd import checkpoint
+    from odelib_amd.engine import check_resume, rng_record
+    rs = np.random.RandomState(3)
+    W, P = 6, 5
+    base = {"theta": rs.rand(P, W), "y0": rs.rand(4, W), "final": rs.rand(4, W),
+            "status": np.zeros(W, np.int32), "next_it": 9}
+    walk = np.ones(P, np.uint8)
+
+    # philox
+    res = dict(base, rng_state=rng_record("philox", 11, 64, 0.05, walk, 20, nits=9))
+    checkpoint.save(tmp_path / "p.npz", res)
+    back = checkpoint.load(tmp_path / "p.npz")
+    assert back["rng_state"] == res["rng_state"]
+    check_resume(back, rng_record("philox", 11, 64, 0.05, walk, 20, nits=30))
+    for bad in (rng_record("philox", 12, 64, 0.05, walk, 20), rng_record("philox", 11, 0, 0.05, walk, 20),
+                rng_record("numpy", 11, 64, 0.05, walk, 20), rng_record("philox", 11, 64, 0.1, walk, 20),
+                rng_record("philox", 11, 64, 0.05, walk, 21)):
+        with pytest.raises(ValueError):
+            check_resume(back, bad)
+
+    # numpy: seeds and prior draws saved; seeds taken from the checkpoint when omitted
+    seeds = np.arange(W) * 3
+    res = dict(base, rng_state=rng_record("numpy", 0, 0, 0.05, walk, 20, prior_draws=P), numpy_seeds=seeds)
+    checkpoint.save(tmp_path / "n.npz", res)
+    back = checkpoint.load(tmp_path / "n.npz")
+    assert np.array_equal(check_resume(back, rng_record("numpy", 0, 0, 0.05, walk, 20, prior_draws=P)), seeds)
+    with pytest.raises(ValueError):
+        check_resume(back, rng_record("numpy", 0, 0, 0.05, walk, 20, prior_draws=P), numpy_seeds=seeds + 1)
+    with pytest.raises(ValueError):
+        check_resume(back, rng_record("numpy", 0, 0, 0.05, walk, 20, prior_draws=0), numpy_seeds=seeds)
+
+    # replay: rows used by the checkpointed run must be unchanged in the resuming streams
+    dz, u = rs.rand(40, P, W), rs.rand(40, W)
+    res = dict(base, rng_state=rng_record("replay", 0, 0, 0.05, walk, 20, replay=(dz, u), nits=9))
+    checkpoint.save(tmp_path / "r.npz", res)
+    back = checkpoint.load(tmp_path / "r.npz")
+    ok = rng_record("replay", 0, 0, 0.05, walk, 20, replay=(dz, u), nits=40)
+    check_resume(back, dict(ok, _replay=(dz, u)))
+    dz2 = dz.copy()
+    dz2[7, 1, 2] += 1e-12
+    with pytest.raises(ValueError):
+        check_resume(back, dict(rng_record("replay", 0, 0, 0.05, walk, 20, replay=(dz2, u), nits=40),
+                                _replay=(dz2, u)))
+    # a checkpoint without recorded state cannot be verified
+    checkpoint.save(tmp_path / "old.npz", base)
+    with pytest.raises(ValueError):
+        check_resume(checkpoint.load(tmp_path / "old.npz"), ok)
+
+
+def test_resolution_never_binds_a_builtin_by_probing_alone():
+    """callables that agree with a built-in on probe points but differ by a
+    term switched on by t (dosing after t=3) or by a state threshold must NOT be
+    replaced by the built-in; they go to the exact transpiled (hipRTC) path."""
+    two_i = CONFIGS["two_i"]["ode"]
+
+    def dosed(y, t, ps):  # forcing only at t > 3 (outside the old probe window)
+        mu, phi, beta, lam, tau = ps[0], ps[1], ps[2], ps[3], ps[4]
+        S, I1, I2, V = y[0], y[1], y[2], y[3]
+        dose = 1e6 if t > 3.5 else 0.0
+        return np.array([mu * S - phi * S * V, phi * S * V - tau * I1, tau * I1 - lam * I2,
+                         beta * lam * I2 - phi * S * V + dose])
+
+    def threshold(y, t, ps):  # extra decay only for tiny susceptible populations
+        mu, phi, beta, lam, tau = ps[0], ps[1], ps[2], ps[3], ps[4]
+        S, I1, I2, V = y[0], y[1], y[2], y[3]
+        dS = mu * S - phi * S * V - (0.5 * S if S < 1e-3 else 0.0)
+        return np.array([dS, phi * S * V - tau * I1, tau * I1 - lam * I2, beta * lam * I2 - phi * S * V])
+
+    def reordered(y, t, ps):  # algebraically two_i, written differently: still the built-in
+        S, I1, I2, V = y
+        mu, phi, beta, lam, tau = ps
+        inf = phi * V * S
+        return [S * mu - inf, inf - I1 * tau, -(lam * I2) + tau * I1, (beta * I2) * lam - inf]
+
+    times = np.linspace(0, 6, 1000)
+    for f in (dosed, threshold):
+        dm = models.resolve_model(f, 4, 5, times=times)
+        assert dm.model_id is None and dm.source is not None, f.__name__
+        with pytest.raises(NotImplementedError):
+            models.resolve(f, 4, 5, times=times)
+        with pytest.raises(ValueError):  # an explicit claim is checked exactly too
+            models.resolve_model(f, 4, 5, device_model="two_i", times=times)
+    assert models.resolve(reordered, 4, 5) == (N.OE_MODEL_TWO_I, 4)
+    assert models.resolve_model(two_i, 4, 5).model_id == N.OE_MODEL_TWO_I
+
+
+def test_untranspilable_callable_is_bound_only_on_request():
+    """A callable outside the transpilable subset cannot be proven equal to a built-in:
+    it is refused unless the caller names the built-in (numerically checked over the
+    whole time grid, with a warning)."""
+    import functools
+
+    def _inf(phi, S, V):
+        return phi * S * V
+
+    def helper_style(y, t, ps):  # calls a user helper: not transpilable
+        mu, phi, beta, lam, tau = ps[0], ps[1], ps[2], ps[3], ps[4]
+        S, I1, I2, V = y[0], y[1], y[2], y[3]
+        i = _inf(phi, S, V)
+        return np.array([mu * S - i, i - tau * I1, tau * I1 - lam * I2, beta * lam * I2 - i])
+
+    with pytest.raises(NotImplementedError, match="cannot be transpiled"):
+        models.resolve_model(helper_style, 4, 5)
+    with pytest.warns(UserWarning, match="numerically only"):
+        assert models.resolve(helper_style, 4, 5, device_model="two_i") == (N.OE_MODEL_TWO_I, 4)
+    late = functools.partial(lambda y, t, ps, k: helper_style(y, t, ps) + (k if t > 4 else 0.0), k=1.0)
+    with pytest.raises(ValueError):
+        models.resolve(late, 4, 5, device_model="two_i", times=np.linspace(0, 6, 100))
