@@ -16,6 +16,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", nargs="+", default=["two_i:rk4:65536", "two_i:dopri5:65536"])
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--modes", nargs="+", default=["traj", "notraj", "traj_half", "traj_noxcd"],
+                    help="traj/notraj + optional _half, _noxcd, _stab (scalar-load step table)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -31,15 +33,15 @@ def main():
         y0 = torch.as_tensor(np.repeat(y0h[:, None], W, axis=1), device=dev).contiguous()
         traj = eng.empty_traj(W)
         row = {"case": case}
-        modes = ("traj", "notraj", "traj_half", "traj_noxcd")
+        modes = tuple(args.modes)
         ms = {k: [] for k in modes}
         # interleaved rounds after a warm-up of every mode (clocks settle, pages mapped)
         for r in range(args.reps + 3):
             for mode in modes:
                 eng.integrate(y0, theta, trajectory=mode.startswith("traj"),
                               traj_out=traj if mode.startswith("traj") else None, sync=True,
-                              half_waves=mode.endswith("half"),
-                              xcd_remap=not mode.endswith("noxcd"))
+                              half_waves="half" in mode, xcd_remap="noxcd" not in mode,
+                              lds_table="stab" not in mode)
                 if r >= 3:
                     ms[mode].append(eng.last_kernel_ms())
         for mode in modes:
