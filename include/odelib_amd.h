@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define OE_ABI_VERSION 2
+#define OE_ABI_VERSION 3
 
 /* return codes */
 enum {
@@ -56,9 +56,14 @@ enum {
 
 /* integrators */
 enum {
-  OE_METHOD_RK4 = 0,   /* fixed-step classical RK4, rk4_substeps steps per output interval */
-  OE_METHOD_DOPRI5 = 1 /* Dormand–Prince 5(4), wavefront-shared step, max-norm error,
-                          dense output onto the times grid */
+  OE_METHOD_RK4 = 0,    /* fixed-step classical RK4, rk4_substeps steps per output interval */
+  OE_METHOD_DOPRI5 = 1, /* Dormand–Prince 5(4), wavefront-shared step, max-norm error,
+                           dense output onto the times grid */
+  OE_METHOD_AUTO = 2,   /* odeint's LSODA behaviour (Framework.py:656): DOPRI5 with a per-walker
+                           stiffness test; stiff or over-budget walkers are integrated again by
+                           the Rosenbrock method (status bit OE_STATUS_STIFF).  n_states <= 8 */
+  OE_METHOD_ROSENBROCK = 3 /* L-stable Rosenbrock 4(3) (ROS4) for every walker, exact Jacobian by
+                              dual numbers, steps ending on every output time.  n_states <= 8 */
 };
 
 /* built-in right-hand sides (demo notebook models + synthetic chain) */
@@ -74,7 +79,8 @@ enum {
 enum {
   OE_STATUS_NONFINITE = 1, /* a state became NaN/inf */
   OE_STATUS_NEGATIVE = 2,  /* a state went negative at an output time */
-  OE_STATUS_MAXSTEP = 4    /* DOPRI5 step budget / step underflow: walker abandoned (NaN output) */
+  OE_STATUS_MAXSTEP = 4,   /* step budget / step underflow: walker abandoned (NaN output) */
+  OE_STATUS_STIFF = 8      /* OE_METHOD_AUTO: the walker was integrated by the stiff method */
 };
 
 /* call flags */

@@ -15,12 +15,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ODELIB_AMD_LIB", os.path.join(_HERE, "csrc", "libodelib_amd.so"))
 
 # --- constants mirrored from include/odelib_amd.h -----------------------------------
-OE_ABI_VERSION = 2
+OE_ABI_VERSION = 3
 OE_OK = 0
-OE_METHOD_RK4, OE_METHOD_DOPRI5 = 0, 1
+OE_METHOD_RK4, OE_METHOD_DOPRI5, OE_METHOD_AUTO, OE_METHOD_ROSENBROCK = 0, 1, 2, 3
 OE_MODEL_ZERO_I, OE_MODEL_ONE_I, OE_MODEL_TWO_I, OE_MODEL_CHAIN = 0, 1, 2, 3
 OE_MODEL_CUSTOM = 1000
-OE_STATUS_NONFINITE, OE_STATUS_NEGATIVE, OE_STATUS_MAXSTEP = 1, 2, 4
+OE_STATUS_NONFINITE, OE_STATUS_NEGATIVE, OE_STATUS_MAXSTEP, OE_STATUS_STIFF = 1, 2, 4, 8
 OE_HOST_PTRS, OE_ASYNC, OE_NT_STORES, OE_PIPE, OE_HALF_WAVES, OE_NO_XCD_REMAP, OE_NO_TIMING = 1, 2, 4, 8, 16, 64, 128
 OE_RNG_REPLAY, OE_RNG_PHILOX, OE_RNG_NUMPY = 0, 1, 2
 

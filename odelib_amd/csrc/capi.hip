@@ -345,13 +345,20 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   for (int i = 1; i < p->n_times; ++i)
     if (!(p->times[i] > p->times[i - 1]))
       return fail(c, OE_ERR_ARG, "oe_problem_set: times must be strictly increasing");
-  if (p->method != OE_METHOD_RK4 && p->method != OE_METHOD_DOPRI5)
+  if (p->method < OE_METHOD_RK4 || p->method > OE_METHOD_ROSENBROCK)
     return fail(c, OE_ERR_ARG, "oe_problem_set: unknown method");
+  if (p->method == OE_METHOD_AUTO || p->method == OE_METHOD_ROSENBROCK) {
+    const bool have = e->rtc ? (e->rtc->n_methods > p->method) : (e->integrate[p->method][0][0] != nullptr);
+    if (!have)
+      return fail(c, OE_ERR_UNSUPPORTED,
+                  "oe_problem_set: the stiff methods (auto, rosenbrock) need n_states <= 8 and a right-hand side "
+                  "that compiles for dual numbers (templated on its scalar type R)");
+  }
   if (p->method == OE_METHOD_RK4 && p->rk4_substeps < 1)
     return fail(c, OE_ERR_ARG, "oe_problem_set: rk4_substeps must be >= 1");
-  if (p->method == OE_METHOD_DOPRI5 &&
+  if (p->method != OE_METHOD_RK4 &&
       (!(p->rtol > 0.0) || !(p->atol >= 0.0) || p->max_steps < 2))
-    return fail(c, OE_ERR_ARG, "oe_problem_set: DOPRI5 needs rtol > 0, atol >= 0, max_steps >= 2");
+    return fail(c, OE_ERR_ARG, "oe_problem_set: adaptive methods need rtol > 0, atol >= 0, max_steps >= 2");
   if (p->n_obs < 0) return fail(c, OE_ERR_ARG, "oe_problem_set: n_obs < 0");
   if (p->n_obs > 0 && (!p->obs_tidx || !p->obs_mask || !p->obs_log || !p->obs_logsigma || !p->obs_lin))
     return fail(c, OE_ERR_ARG, "oe_problem_set: observation arrays missing");

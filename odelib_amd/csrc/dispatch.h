@@ -16,10 +16,10 @@ struct Entry {
   int32_t model_id;
   int32_t S;
   int32_t P;  // the model's own parameter count
-  // [method][traj][nt]
-  IntegrateLaunch integrate[2][2][2];
+  // [method][traj][nt]; methods kAuto / kRos4 are null when S > kStiffMaxS
+  IntegrateLaunch integrate[4][2][2];
   IntegrateLaunch rk4_piped[2];  // [nt]; null when S > 8 (LDS ring too large)
-  MHLaunch mh[2];
+  MHLaunch mh[4];
   const RtcModule* rtc = nullptr;  // user RHS compiled at run time (launchers above unused)
 };
 
@@ -60,26 +60,31 @@ void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream
   hipLaunchKernelGGL((k_mh<M, METHOD>), g, b, 0, s, pb, ma);
 }
 
+template <class M, int METHOD>
+void fill_method(Entry& e) {
+  e.integrate[METHOD][0][0] = launch_integrate<M, METHOD, false, false>;
+  e.integrate[METHOD][0][1] = launch_integrate<M, METHOD, false, false>;  // NT only matters with a trajectory
+  e.integrate[METHOD][1][0] = launch_integrate<M, METHOD, true, false>;
+  e.integrate[METHOD][1][1] = launch_integrate<M, METHOD, true, true>;
+  e.mh[METHOD] = launch_mh<M, METHOD>;
+}
+
 template <class M>
 Entry make_entry(int32_t model_id) {
   Entry e{};
   e.model_id = model_id;
   e.S = M::S;
   e.P = M::P;
-  e.integrate[0][0][0] = launch_integrate<M, 0, false, false>;
-  e.integrate[0][1][0] = launch_integrate<M, 0, true, false>;
-  e.integrate[0][1][1] = launch_integrate<M, 0, true, true>;
-  e.integrate[0][0][1] = launch_integrate<M, 0, false, false>;
-  e.integrate[1][0][0] = launch_integrate<M, 1, false, false>;
-  e.integrate[1][1][0] = launch_integrate<M, 1, true, false>;
-  e.integrate[1][1][1] = launch_integrate<M, 1, true, true>;
-  e.integrate[1][0][1] = launch_integrate<M, 1, false, false>;
+  fill_method<M, kRK4>(e);
+  fill_method<M, kDOPRI5>(e);
+  if constexpr (M::S <= kStiffMaxS) {
+    fill_method<M, kAuto>(e);
+    fill_method<M, kRos4>(e);
+  }
   if constexpr (M::S <= 8) {
     e.rk4_piped[0] = launch_rk4_piped<M, false>;
     e.rk4_piped[1] = launch_rk4_piped<M, true>;
   }
-  e.mh[0] = launch_mh<M, 0>;
-  e.mh[1] = launch_mh<M, 1>;
   return e;
 }
 

@@ -55,7 +55,12 @@ struct DevProblem {
   double sstot;         // R² denominator
 };
 
-enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4 };
+enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8 };
+
+// integrators (OE_METHOD_*): fixed-step RK4, DOPRI5, DOPRI5 with stiffness detection and
+// the Rosenbrock fallback for stiff / over-budget walkers (LSODA-like), Rosenbrock only
+enum : int { kRK4 = 0, kDOPRI5 = 1, kAuto = 2, kRos4 = 3 };
+constexpr int kStiffMaxS = 8;  // the stiff methods factor an S x S matrix per lane in registers
 
 // per-lane accumulators of the fused likelihood
 struct Acc {
@@ -393,8 +398,11 @@ __device__ __forceinline__ double inv_fifth_root(double x) {
 }
 }  // namespace dp
 
-template <class M, int PMAX, bool TRAJ, bool NT>
-__device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
+// AUTO: Hairer's stiffness test on every accepted step (h·|λ| estimated from the last two
+// stages, ≥ 3.25 on 15 accepted steps in a row evicts the lane, as does the step
+// budget); returns whether this (active) lane was evicted, i.e. needs the stiff method.
+template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false>
+__device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, uint32_t off, bool active, Acc& a) {
   using namespace dp;
@@ -453,6 +461,7 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
   double t_obs = (nxt < pb.T) ? times[nxt] : __builtin_inf();        // and its time
   int nst = 0;  // steps since the last grid point
   bool last_rej = false;
+  int n_stiff = 0, n_nonstiff = 0;  // AUTO: consecutive stiff / non-stiff accepted steps
   while (i < pb.T) {
     bool last = false;
     if (t + h >= tend) { h = tend - t; last = true; }
@@ -504,6 +513,28 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
     ++nst;
 
     if (err <= 1.0) {
+      if constexpr (AUTO) {
+        // stiffness: h²·Σ(k7−k6)² > 3.25²·Σ(ynew − y6)² (y6 = the stage-6 input), i.e.
+        // h·|λ| > 3.25 (Hairer & Wanner I, §II.10); exact products, no square root
+        double stnum = 0.0, stden = 0.0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const double dk = k7[s] - k6[s], dy = yn[s] - yt[s];
+          stnum = fma(dk, dk, stnum);
+          stden = fma(dy, dy, stden);
+        }
+        if (stden > 0.0 && (h * h) * stnum > 10.5625 * stden) {
+          n_nonstiff = 0;
+          ++n_stiff;
+        } else if (++n_nonstiff >= 6) {
+          n_stiff = 0;
+        }
+        if (!dead && n_stiff >= 15) {  // hand the walker to the stiff method
+          dead = true;
+#pragma unroll
+          for (int s = 0; s < S; ++s) { yn[s] = __builtin_nan(""); k7[s] = __builtin_nan(""); }
+        }
+      }
       const double tn = last ? tend : t + h;
       // Dense output for every grid point in (t, tn] from Hairer's coefficients
       // ydf, bsp, r4, r5.  Trajectory mode: formed eagerly once per accepted step (a grid
@@ -610,15 +641,43 @@ __device__ __forceinline__ void integrate_dopri5(const DevProblem& pb, double (&
   if (dead && active) a.status |= ST_MAXSTEP;
   check_finite(y, a);
   if (kLean && dead) a.nf = __builtin_nan("");  // as if poisoned: final state non-finite
+  return dead && active;
 }
+
+}  // namespace oe
+#include "stiff.cuh"
+namespace oe {
 
 template <class M, int PMAX, int METHOD, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, int64_t w, bool active, Acc& a) {
   const uint32_t off = (uint32_t)w * 8u;  // byte offset of walker w in a [..][W] row
-  if constexpr (METHOD == 0) integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
-  else integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  if constexpr (METHOD == kRK4) {
+    integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  } else if constexpr (METHOD == kDOPRI5 || M::S > kStiffMaxS) {
+    integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  } else if constexpr (METHOD == kAuto) {
+    // LSODA-like: DOPRI5 with the stiffness test; walkers it evicts (stiff, or over the
+    // step budget) are integrated again from their initial state by the Rosenbrock
+    // method, their likelihood accumulated afresh (status bit ST_STIFF)
+    constexpr int S = M::S;
+    double yi[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) yi[s] = y[s];
+    const bool redo = integrate_dopri5<M, PMAX, TRAJ, NT, true>(pb, y, p, traj, W, off, active, a);
+    if (__ballot(redo) != 0ull) {  // wave-uniform
+      if (redo) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) y[s] = yi[s];
+        a = acc_init();
+        a.status = ST_STIFF;
+      }
+      integrate_ros4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, redo, a);
+    }
+  } else {  // kRos4: the Rosenbrock method for every walker
+    integrate_ros4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, active, a);
+  }
 }
 
 // ---------------------------------------------------------------------------------

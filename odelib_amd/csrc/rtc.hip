@@ -21,7 +21,7 @@
 
 namespace oe {
 
-static const char* kMethodName[2] = {"0", "1"};
+static const char* kMethodName[4] = {"0", "1", "2", "3"};
 static const char* kBool[2] = {"false", "true"};
 
 std::string rtc_integrate_name(int method, int traj, int nt) {
@@ -29,7 +29,7 @@ std::string rtc_integrate_name(int method, int traj, int nt) {
 }
 std::string rtc_mh_name(int method) { return std::string("oe::k_mh<UserModel, ") + kMethodName[method] + ">"; }
 
-std::string rtc_source(const std::string& body, int S, int P) {
+std::string rtc_source(const std::string& body, int S, int P, int n_methods) {
   std::string src;
   src += "typedef unsigned long long uint64_t; typedef long long int64_t;\n";
   src += "typedef unsigned int uint32_t; typedef int int32_t;\n";
@@ -41,7 +41,7 @@ std::string rtc_source(const std::string& body, int S, int P) {
   src += "    (void)t;\n";
   src += body;
   src += "\n  }\n};\n";
-  for (int m = 0; m < 2; ++m) {
+  for (int m = 0; m < n_methods; ++m) {
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)
         src += "template __global__ void " + rtc_integrate_name(m, tr, nt) + "(const oe::DevProblem, const oe::IntegrateArgs);\n";
@@ -87,22 +87,33 @@ static int compile_program(const std::string& src, const char* arch, std::vector
   return 0;
 }
 
-static std::vector<std::string> all_names() {
+static std::vector<std::string> all_names(int n_methods) {
   std::vector<std::string> names;
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < n_methods; ++m)
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_integrate_name(m, tr, nt));
-  for (int m = 0; m < 2; ++m) names.push_back(rtc_mh_name(m));
+  for (int m = 0; m < n_methods; ++m) names.push_back(rtc_mh_name(m));
   return names;
 }
 
 int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule* out, std::string& err) {
-  std::vector<std::string> names = all_names(), lowered;
+  int n_methods = S <= kStiffMaxS ? 4 : 2;
+  std::vector<std::string> names = all_names(n_methods), lowered;
   std::vector<char> code;
   std::string log;
-  if (compile_program(rtc_source(body, S, P), arch, names, lowered, code, log)) {
-    err = "hipRTC compilation of the user RHS failed:\n" + log;
-    return -1;
+  if (compile_program(rtc_source(body, S, P, n_methods), arch, names, lowered, code, log)) {
+    if (n_methods == 2) {
+      err = "hipRTC compilation of the user RHS failed:\n" + log;
+      return -1;
+    }
+    // a body that only compiles for double (no dual-number Jacobian): no stiff methods
+    n_methods = 2;
+    names = all_names(n_methods);
+    std::string log2;
+    if (compile_program(rtc_source(body, S, P, n_methods), arch, names, lowered, code, log2)) {
+      err = "hipRTC compilation of the user RHS failed:\n" + log2;
+      return -1;
+    }
   }
   if (!out) return 0;  // compile check only
   hipModule_t mod;
@@ -111,15 +122,16 @@ int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule
     return -1;
   }
   out->mod = mod;
+  out->n_methods = n_methods;
   int idx = 0;
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < n_methods; ++m)
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)
         if (hipModuleGetFunction(&out->integrate[m][tr][nt], mod, lowered[idx++].c_str()) != hipSuccess) {
           err = "hipModuleGetFunction failed";
           return -1;
         }
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < n_methods; ++m)
     if (hipModuleGetFunction(&out->mh[m], mod, lowered[idx++].c_str()) != hipSuccess) {
       err = "hipModuleGetFunction failed";
       return -1;

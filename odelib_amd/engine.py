@@ -21,7 +21,8 @@ import numpy as np
 
 from . import _native as N
 
-METHODS = {"rk4": N.OE_METHOD_RK4, "dopri5": N.OE_METHOD_DOPRI5}
+METHODS = {"rk4": N.OE_METHOD_RK4, "dopri5": N.OE_METHOD_DOPRI5, "auto": N.OE_METHOD_AUTO,
+           "rosenbrock": N.OE_METHOD_ROSENBROCK}
 ODEINT_TOL = 1.49012e-8  # scipy.integrate.odeint default rtol/atol (Framework.py:656)
 
 

@@ -843,7 +843,7 @@ def transpile(func, n_states: int, n_params: int) -> TranspiledRHS:
         if name in declared:
             lines.append(f"v_{name} = {_c(expr)};")
         else:
-            lines.append(f"double v_{name} = {_c(expr)};")
+            lines.append(f"R v_{name} = {_c(expr)};")  # R: double, or a dual number for the Jacobian
             declared.add(name)
     for k, e in enumerate(tr.outs):
         lines.append(f"dy[{k}] = {_c(e)};")

@@ -15,7 +15,12 @@
  *   - the fused likelihood: chi = Σ finite (O − log C)²/(2S²) (stats.py:41),
  *     ssres = Σ non-NaN (C − exp O)² (stats.py:52);
  *   - the batched Metropolis–Hastings step (Samplers.py:104-153) with replay or
- *     Philox4x32-10 draws.
+ *     Philox4x32-10 draws;
+ *   - the stiff methods: DOPRI5 with Hairer's stiffness test and
+ *     eviction ('auto'), and the L-stable ROS4 Rosenbrock method (Hairer & Wanner II
+ *     §IV.7) with the Jacobian from forward-mode dual numbers through the model RHS,
+ *     LU with partial pivoting, steps ending on every grid time, for 64-lane groups
+ *     sharing one step size.
  */
 #include <math.h>
 #include <stdint.h>
@@ -27,7 +32,8 @@
 #define MAXP 80
 
 enum { M_ZERO_I = 0, M_ONE_I = 1, M_TWO_I = 2, M_CHAIN = 3 };
-enum { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4 };
+enum { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8 };
+enum { METHOD_RK4 = 0, METHOD_DOPRI5 = 1, METHOD_AUTO = 2, METHOD_ROS4 = 3 };
 
 typedef struct {
   int model, S, P, T;
@@ -179,6 +185,9 @@ typedef struct {
   int64_t w;
   Acc a;
   int kobs;
+  int n_stiff, n_nonstiff; /* auto: consecutive stiff / non-stiff accepted steps */
+  int part;                /* ros4: lane takes part in the stiff integration */
+  double y0c[MAXS];        /* auto: initial state, for the restart */
 } Lane;
 
 /* x^(-1/5), same operations as ode_kernels.cuh inv_fifth_root (bit-identical) */
@@ -207,14 +216,16 @@ static double grp_max(Lane* L, int n, int use_dead_zero) {
   return m;
 }
 
-/* lanes: up to 64; y in L[l].y; p[l*MAXP ...] */
-static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
+/* lanes: up to 64; y in L[l].y; p[l*MAXP ...].  auto: Hairer's stiffness test on every
+   accepted step; 15 stiff steps in a row evict the lane (as the step budget does) */
+static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W, int autom) {
   const int S = pb->S;
   const double t0 = pb->times[0], tend = pb->times[pb->T - 1];
   const double rtol = pb->rtol, atol = pb->atol;
   for (int l = 0; l < nl; ++l) {
     L[l].dead = !L[l].active;
     L[l].kobs = 0;
+    L[l].n_stiff = L[l].n_nonstiff = 0;
     emit(pb, 0, L[l].y, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
     rhs(pb, L[l].y, t0, p + l * MAXP, L[l].k1);
   }
@@ -295,6 +306,27 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     double err = grp_max(L, nl, 1);
     ++nst;
     if (err <= 1.0) {
+      if (autom) {
+        for (int l = 0; l < nl; ++l) {
+          Lane* q = &L[l];
+          double stnum = 0.0, stden = 0.0;
+          for (int s = 0; s < S; ++s) {
+            double dk = q->k7[s] - q->k6[s], dy = q->yn[s] - q->yt[s];
+            stnum = fma(dk, dk, stnum);
+            stden = fma(dy, dy, stden);
+          }
+          if (stden > 0.0 && (h * h) * stnum > 10.5625 * stden) {
+            q->n_nonstiff = 0;
+            ++q->n_stiff;
+          } else if (++q->n_nonstiff >= 6) {
+            q->n_stiff = 0;
+          }
+          if (!q->dead && q->n_stiff >= 15) {
+            q->dead = 1;
+            for (int s = 0; s < S; ++s) q->yn[s] = q->k7[s] = NAN;
+          }
+        }
+      }
       double tn = last ? tend : t + h;
       const double rh = 1.0 / h;
       const double hd1 = h * d1, hd3 = h * d3, hd4 = h * d4, hd5 = h * d5, hd6 = h * d6, hd7 = h * d7;
@@ -365,6 +397,330 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
   }
 }
 
+
+/* ---- stiff methods ---- */
+
+/* forward-mode dual number: value + n tangents (n = S + 1: the states, then t) */
+typedef struct {
+  double v;
+  double d[MAXS + 1];
+} Dl;
+
+static Dl dl_c(double x, int n) {
+  Dl r;
+  r.v = x;
+  for (int i = 0; i < n; ++i) r.d[i] = 0.0;
+  return r;
+}
+static Dl dl_neg(Dl a, int n) {
+  Dl r;
+  r.v = -a.v;
+  for (int i = 0; i < n; ++i) r.d[i] = -a.d[i];
+  return r;
+}
+static Dl dl_mul(Dl a, Dl b, int n) {
+  Dl r;
+  r.v = a.v * b.v;
+  for (int i = 0; i < n; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i];
+  return r;
+}
+static Dl dl_fma(Dl a, Dl b, Dl c, int n) {
+  Dl r;
+  r.v = fma(a.v, b.v, c.v);
+  for (int i = 0; i < n; ++i) r.d[i] = (a.d[i] * b.v + a.v * b.d[i]) + c.d[i];
+  return r;
+}
+
+/* the built-in right-hand sides over dual numbers, operation for operation as rhs() */
+static void dual_rhs(const Prob* pb, const Dl* y, const Dl* ps, Dl* dy, int n) {
+  const int N = pb->S;
+  switch (pb->model) {
+    case M_ZERO_I: {
+      Dl mu = ps[0], phi = ps[1], beta = ps[2];
+      Dl Sv = y[0], V = y[1];
+      Dl inf = dl_mul(dl_mul(phi, Sv, n), V, n);
+      dy[0] = dl_fma(mu, Sv, dl_neg(inf, n), n);
+      dy[1] = dl_fma(beta, inf, dl_neg(inf, n), n);
+      break;
+    }
+    case M_ONE_I: {
+      Dl mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3];
+      Dl Sv = y[0], I1 = y[1], V = y[2];
+      Dl inf = dl_mul(dl_mul(phi, Sv, n), V, n);
+      dy[0] = dl_fma(mu, Sv, dl_neg(inf, n), n);
+      dy[1] = dl_fma(dl_neg(lam, n), I1, inf, n);
+      dy[2] = dl_fma(dl_mul(beta, lam, n), I1, dl_neg(inf, n), n);
+      break;
+    }
+    case M_TWO_I: {
+      Dl mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3], tau = ps[4];
+      Dl Sv = y[0], I1 = y[1], I2 = y[2], V = y[3];
+      Dl inf = dl_mul(dl_mul(phi, Sv, n), V, n);
+      dy[0] = dl_fma(mu, Sv, dl_neg(inf, n), n);
+      dy[1] = dl_fma(dl_neg(tau, n), I1, inf, n);
+      dy[2] = dl_fma(tau, I1, dl_neg(dl_mul(lam, I2, n), n), n);
+      dy[3] = dl_fma(dl_mul(beta, lam, n), I2, dl_neg(inf, n), n);
+      break;
+    }
+    default: {
+      Dl mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3], tau = ps[4];
+      Dl Sv = y[0], V = y[N - 1];
+      Dl inf = dl_mul(dl_mul(phi, Sv, n), V, n);
+      dy[0] = dl_fma(mu, Sv, dl_neg(inf, n), n);
+      dy[1] = dl_fma(dl_neg(tau, n), y[1], inf, n);
+      for (int k = 2; k <= N - 3; ++k) dy[k] = dl_fma(tau, y[k - 1], dl_neg(dl_mul(tau, y[k], n), n), n);
+      dy[N - 2] = dl_fma(tau, y[N - 3], dl_neg(dl_mul(lam, y[N - 2], n), n), n);
+      dy[N - 1] = dl_fma(dl_mul(beta, lam, n), y[N - 2], dl_neg(inf, n), n);
+    }
+  }
+}
+
+/* f, J = df/dy (row s = df_s) and df/dt at (t, y) */
+static void jac_eval(const Prob* pb, const double* y, double t, const double* p, double* f, double* J, double* ft) {
+  const int S = pb->S, n = S + 1;
+  Dl yd[MAXS], pd[MAXP], fd[MAXS];
+  for (int s = 0; s < S; ++s) { yd[s] = dl_c(y[s], n); yd[s].d[s] = 1.0; }
+  Dl td = dl_c(t, n);
+  td.d[S] = 1.0;
+  (void)td; /* the built-in models are autonomous: t enters no product */
+  for (int j = 0; j < MAXP; ++j) pd[j] = dl_c(p[j], n);
+  dual_rhs(pb, yd, pd, fd, n);
+  for (int s = 0; s < S; ++s) {
+    f[s] = fd[s].v;
+    for (int j = 0; j < S; ++j) J[s * S + j] = fd[s].d[j];
+    ft[s] = fd[s].d[S];
+  }
+}
+
+/* ROS4, L-stable set (Hairer & Wanner II §IV.7), Kaps-Rentrop form */
+static const double r_gam = 0.57282, r_a21 = 2.0, r_a31 = 1.867943637803922, r_a32 = 0.2344449711399156,
+                    r_c21 = -7.137615036412310, r_c31 = 2.580708087951457, r_c32 = 0.6515950076447975,
+                    r_c41 = -2.137148994382534, r_c42 = -0.3214669691237626, r_c43 = -0.6949742501781779,
+                    r_m1 = 2.255570073418735, r_m2 = 0.2870493262186792, r_m3 = 0.435317943184018,
+                    r_m4 = 1.093502252409163, r_e1 = -0.2815431932141155, r_e2 = -0.0727619912493892,
+                    r_e3 = -0.1082196201495311, r_e4 = -1.093502252409163, r_a2x = 1.14564,
+                    r_a3x = 0.65521686381559, r_g1x = 0.57282, r_g2x = -1.769193891319233,
+                    r_g3x = 0.7592633437920482, r_g4x = -0.104902108710045;
+
+/* x^(-1/4), same operations as stiff.cuh inv_fourth_root (bit-identical) */
+static double inv_fourth_root(double x) {
+  int e;
+  const double m = frexp(x, &e);
+  int q = e / 4, r = e % 4;
+  if (r < 0) { r += 4; q -= 1; }
+  double y = fma(fma(0.3171, m, -0.8457), m, 1.5304);
+  for (int it = 0; it < 3; ++it) {
+    const double y2 = y * y;
+    y = (y * fma(-m, y2 * y2, 5.0)) * 0.25;
+  }
+  const double c = r == 0 ? 1.0 : r == 1 ? 0.8408964152537145 : r == 2 ? 0.7071067811865476 : 0.5946035575013605;
+  return ldexp(c * y, -q);
+}
+
+double ref_inv_fourth_root(double x) { return inv_fourth_root(x); }
+
+/* LU with partial pivoting (first maximum, full-row interchanges), a is S x S row-major */
+static void lu_factor(int S, double* a, int* piv, double* dinv) {
+  for (int k = 0; k < S; ++k) {
+    int pk = k;
+    double best = fabs(a[k * S + k]);
+    for (int i = k + 1; i < S; ++i) {
+      double v = fabs(a[i * S + k]);
+      if (v > best) { best = v; pk = i; }
+    }
+    piv[k] = pk;
+    if (pk != k)
+      for (int j = 0; j < S; ++j) { double tmp = a[k * S + j]; a[k * S + j] = a[pk * S + j]; a[pk * S + j] = tmp; }
+    const double inv = 1.0 / a[k * S + k];
+    dinv[k] = inv;
+    for (int i = k + 1; i < S; ++i) {
+      const double l = a[i * S + k] * inv;
+      a[i * S + k] = l;
+      for (int j = k + 1; j < S; ++j) a[i * S + j] = fma(-l, a[k * S + j], a[i * S + j]);
+    }
+  }
+}
+
+static void lu_solve(int S, const double* a, const int* piv, const double* dinv, double* b) {
+  for (int k = 0; k < S; ++k)
+    if (piv[k] != k) { double tmp = b[k]; b[k] = b[piv[k]]; b[piv[k]] = tmp; }
+  for (int k = 0; k < S; ++k)
+    for (int i = k + 1; i < S; ++i) b[i] = fma(-a[i * S + k], b[k], b[i]);
+  for (int k = S - 1; k >= 0; --k) {
+    double x = b[k];
+    for (int j = k + 1; j < S; ++j) x = fma(-a[k * S + j], b[j], x);
+    b[k] = x * dinv[k];
+  }
+}
+
+typedef struct {
+  double f0[MAXS], J[MAXS * MAXS], ft[MAXS], y1[MAXS];
+} RosLane;
+
+/* Rosenbrock over a 64-lane group: lanes with part set integrate from their L[l].y,
+   the others sit out (no emit, no vote on the step size) */
+static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
+  static __thread RosLane R[LANES];
+  const int S = pb->S;
+  const double t0 = pb->times[0], tend = pb->times[pb->T - 1];
+  const double rtol = pb->rtol, atol = pb->atol;
+  double t = t0;
+  for (int l = 0; l < nl; ++l) {
+    Lane* q = &L[l];
+    q->dead = !q->part;
+    q->kobs = 0;
+    if (q->part) emit(pb, 0, q->y, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
+    jac_eval(pb, q->y, t, p + l * MAXP, R[l].f0, R[l].J, R[l].ft);
+  }
+  double h = INFINITY;
+  for (int l = 0; l < nl; ++l) {
+    Lane* q = &L[l];
+    double d0 = 0.0, d1v = 0.0;
+    for (int s = 0; s < S; ++s) {
+      double sk = atol + rtol * fabs(q->y[s]);
+      d0 = fmax(d0, fabs(q->y[s]) / sk);
+      d1v = fmax(d1v, fabs(R[l].f0[s]) / sk);
+    }
+    double h0 = (d0 <= 1e-5 || d1v <= 1e-5) ? 1e-6 : 0.01 * (d0 / d1v);
+    h0 = fmin(h0, tend - t0);
+    double yt[MAXS], f1[MAXS];
+    for (int s = 0; s < S; ++s) yt[s] = fma(h0, R[l].f0[s], q->y[s]);
+    rhs(pb, yt, t + h0, p + l * MAXP, f1);
+    double d2 = 0.0;
+    for (int s = 0; s < S; ++s) {
+      double sk = atol + rtol * fabs(q->y[s]);
+      d2 = fmax(d2, fabs(f1[s] - R[l].f0[s]) / sk);
+    }
+    d2 = d2 / h0;
+    double dm = fmax(d1v, d2);
+    double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : inv_fourth_root(dm / 0.01);
+    double hl = fmin(100.0 * h0, h1);
+    if (q->dead || !isfinite(hl) || !(hl > 0.0)) hl = tend - t0;
+    h = fmin(h, hl);
+  }
+  h = fmin(h, tend - t0);
+  const double span = tend - t0;
+  const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
+  const double inv_gam = 1.0 / r_gam;
+  const int budget = 8 * pb->max_steps; /* stiff.cuh kRosBudget */
+  int i = 1, nst = 0, last_rej = 0;
+  while (i < pb->T) {
+    const double ti = pb->times[i];
+    const double hp = h;
+    int clip = 0;
+    if (t + h >= ti) { h = ti - t; clip = 1; }
+    const double rh = 1.0 / h, gh = rh * inv_gam;
+    const double c21h = r_c21 * rh, c31h = r_c31 * rh, c32h = r_c32 * rh, c41h = r_c41 * rh, c42h = r_c42 * rh,
+                 c43h = r_c43 * rh;
+    const double hg1 = h * r_g1x, hg2 = h * r_g2x, hg3 = h * r_g3x, hg4 = h * r_g4x;
+    for (int l = 0; l < nl; ++l) {
+      Lane* q = &L[l];
+      RosLane* rl = &R[l];
+      const double* pl = p + l * MAXP;
+      double lu[MAXS * MAXS], dinv[MAXS];
+      int piv[MAXS];
+      for (int r = 0; r < S; ++r)
+        for (int c = 0; c < S; ++c) lu[r * S + c] = (r == c) ? gh - rl->J[r * S + c] : -rl->J[r * S + c];
+      lu_factor(S, lu, piv, dinv);
+      double g1[MAXS], g2[MAXS], g3[MAXS], g4[MAXS], yt[MAXS], fv[MAXS];
+      for (int s = 0; s < S; ++s) g1[s] = fma(hg1, rl->ft[s], rl->f0[s]);
+      lu_solve(S, lu, piv, dinv, g1);
+      for (int s = 0; s < S; ++s) yt[s] = fma(r_a21, g1[s], q->y[s]);
+      rhs(pb, yt, t + r_a2x * h, pl, fv);
+      for (int s = 0; s < S; ++s) g2[s] = fma(hg2, rl->ft[s], fma(c21h, g1[s], fv[s]));
+      lu_solve(S, lu, piv, dinv, g2);
+      for (int s = 0; s < S; ++s) yt[s] = fma(r_a32, g2[s], fma(r_a31, g1[s], q->y[s]));
+      rhs(pb, yt, t + r_a3x * h, pl, fv);
+      for (int s = 0; s < S; ++s) g3[s] = fma(hg3, rl->ft[s], fma(c32h, g2[s], fma(c31h, g1[s], fv[s])));
+      lu_solve(S, lu, piv, dinv, g3);
+      for (int s = 0; s < S; ++s)
+        g4[s] = fma(hg4, rl->ft[s], fma(c43h, g3[s], fma(c42h, g2[s], fma(c41h, g1[s], fv[s]))));
+      lu_solve(S, lu, piv, dinv, g4);
+      double num = 0.0, den = 1.0, nfe = 0.0;
+      for (int s = 0; s < S; ++s) {
+        rl->y1[s] = fma(r_m4, g4[s], fma(r_m3, g3[s], fma(r_m2, g2[s], fma(r_m1, g1[s], q->y[s]))));
+        double e = fma(r_e4, g4[s], fma(r_e3, g3[s], fma(r_e2, g2[s], r_e1 * g1[s])));
+        double ae = fabs(e);
+        double sk = fma(rtol, fmax(fabs(q->y[s]), fabs(rl->y1[s])), atol);
+        nfe = fma(ae, 0.0, nfe);
+        nfe = fma(rl->y1[s], 0.0, nfe);
+        if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
+      }
+      double el = num / den;
+      if (!isfinite(el) || isnan(nfe)) el = 1e30;
+      if (q->dead) el = 0.0;
+      q->el = el;
+    }
+    double err = grp_max(L, nl, 1);
+    ++nst;
+    if (err <= 1.0) {
+      const double tn = clip ? ti : t + h;
+      for (int l = 0; l < nl; ++l)
+        if (L[l].part) memcpy(L[l].y, R[l].y1, sizeof(double) * S);
+      t = tn;
+      if (clip) {
+        for (int l = 0; l < nl; ++l)
+          if (L[l].part) emit(pb, i, L[l].y, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
+        ++i;
+        nst = 0;
+      }
+      if (i < pb->T)
+        for (int l = 0; l < nl; ++l) jac_eval(pb, L[l].y, t, p + l * MAXP, R[l].f0, R[l].J, R[l].ft);
+      double fac = (err > 0.0) ? 0.9 * inv_fourth_root(err) : 6.0;
+      fac = fmin(6.0, fmax(0.2, fac));
+      if (last_rej) fac = fmin(fac, 1.0);
+      const double hn = h * fac;
+      h = clip ? fmax(hn, hp) : hn;
+      last_rej = 0;
+    } else {
+      h = h * fmax(0.2, 0.9 * inv_fourth_root(err));
+      last_rej = 1;
+    }
+    if (nst >= budget || h < hmin) {
+      for (int l = 0; l < nl; ++l)
+        if (!L[l].dead && L[l].el >= 0.5 * err) {
+          L[l].dead = 1;
+          L[l].a.status |= ST_MAXSTEP;
+          for (int s = 0; s < S; ++s) L[l].y[s] = NAN;
+        }
+      nst = budget / 2;
+      int alive = 0;
+      for (int l = 0; l < nl; ++l) alive |= !L[l].dead;
+      if (!alive) {
+        double yo[MAXS];
+        for (int s = 0; s < S; ++s) yo[s] = NAN;
+        for (; i < pb->T; ++i)
+          for (int l = 0; l < nl; ++l)
+            if (L[l].part) emit(pb, i, yo, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
+        break;
+      }
+      if (h < hmin) h = fmin(1e-3 * span, tend - t);
+    }
+  }
+  for (int l = 0; l < nl; ++l)
+    if (L[l].part) check_finite(S, L[l].y, &L[l].a);
+}
+
+/* 'auto': DOPRI5 with the stiffness test, then the evicted walkers again from t0 by ROS4 */
+static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
+  const int S = pb->S;
+  for (int l = 0; l < nl; ++l) memcpy(L[l].y0c, L[l].y, sizeof(double) * S);
+  dopri5_group(pb, L, nl, p, traj, W, 1);
+  int any = 0;
+  for (int l = 0; l < nl; ++l) {
+    L[l].part = L[l].dead && L[l].active;
+    any |= L[l].part;
+  }
+  if (!any) return;
+  for (int l = 0; l < nl; ++l)
+    if (L[l].part) {
+      memcpy(L[l].y, L[l].y0c, sizeof(double) * S);
+      acc_init(&L[l].a);
+      L[l].a.status = ST_STIFF;
+    }
+  ros4_group(pb, L, nl, p, traj, W);
+}
+
 static Prob make_prob(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                       const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                       int substeps, double rtol, double atol, int max_steps) {
@@ -403,8 +759,13 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
     }
     for (int l = 0; l < LANES; ++l)
       if (L[l].active) check_finite(pb->S, L[l].y, &L[l].a);
+  } else if (pb->method == METHOD_DOPRI5) {
+    dopri5_group(pb, L, LANES, p, traj, W, 0);
+  } else if (pb->method == METHOD_AUTO) {
+    auto_group(pb, L, LANES, p, traj, W);
   } else {
-    dopri5_group(pb, L, LANES, p, traj, W);
+    for (int l = 0; l < LANES; ++l) L[l].part = L[l].active;
+    ros4_group(pb, L, LANES, p, traj, W);
   }
   for (int l = 0; l < LANES; ++l) out_acc[l] = L[l].a;
 }

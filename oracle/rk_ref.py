@@ -34,6 +34,8 @@ def lib():
                              i64, i64, i32, i32, i32, u64, d, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ref_inv_fifth_root.restype = d
         L.ref_inv_fifth_root.argtypes = [d]
+        L.ref_inv_fourth_root.restype = d
+        L.ref_inv_fourth_root.argtypes = [d]
         L.ref_philox4x32_10.restype = None
         L.ref_philox4x32_10.argtypes = [vp, vp, vp]
         L.ref_philox_draws.restype = None
@@ -46,7 +48,7 @@ def _p(a):
     return None if a is None else a.ctypes.data
 
 
-METHODS = {"rk4": 0, "dopri5": 1}
+METHODS = {"rk4": 0, "dopri5": 1, "auto": 2, "rosenbrock": 3}
 
 
 class Problem:
@@ -117,6 +119,11 @@ def mh_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, rng="philox"
 def inv_fifth_root(x: float) -> float:
     """x^(-1/5) as the DOPRI5 step controller computes it (oracle/rk_ref.c)."""
     return lib().ref_inv_fifth_root(float(x))
+
+
+def inv_fourth_root(x: float) -> float:
+    """x^(-1/4) as the Rosenbrock step controller computes it (oracle/rk_ref.c)."""
+    return lib().ref_inv_fourth_root(float(x))
 
 
 def philox4x32_10(ctr, key):

@@ -1,0 +1,170 @@
+"""GPU parity of the stiff methods (OE_METHOD_AUTO: DOPRI5 + stiffness test + Rosenbrock
+restart; OE_METHOD_ROSENBROCK) through the C-ABI:
+
+* same algorithm (oracle/rk_ref.c): trajectories and status bitwise, chi rtol 1e-12
+  (ocml vs libm log), on waves that mix the demo draws with stiff ones;
+* reference algorithm: within 1e-6·|y| + 1e-6 of a tight implicit solution (scipy Radau,
+  rtol 1e-13) where odeint's LSODA would have switched to BDF (Framework.py:656);
+* with no stiff walker 'auto' is DOPRI5 bit for bit (C2 size);
+* MH with 'auto' against the C restatement; a user model compiled with hipRTC gets the
+  stiff methods (its Jacobian from dual numbers, including ∂f/∂t of a time forcing).
+"""
+import numpy as np
+import pytest
+from scipy.integrate import solve_ivp
+
+from helpers import CONFIGS, THETA, demo_df, product_model, walker_thetas
+from oracle import rk_ref
+from test_stiff_oracle import STIFF_SETS
+from test_transpile import sat_infection
+
+pytestmark = pytest.mark.gpu
+
+TWO_I_TEMPLATED_BODY = """
+    const R mu = ps[0], phi = ps[1], beta = ps[2], lam = ps[3], tau = ps[4];
+    const R Sv = y[0], I1 = y[1], I2 = y[2], V = y[3];
+    const R inf = phi * Sv * V;
+    dy[0] = fma(mu, Sv, -inf);
+    dy[1] = fma(-tau, I1, inf);
+    dy[2] = fma(tau, I1, -(lam * I2));
+    dy[3] = fma(beta * lam, I2, -inf);
+"""
+
+
+def _mixed_thetas(name, W, stiff_lanes, seed=0):
+    """demo draws with a few lanes replaced by stiff parameter sets (two_i: tau/lam)"""
+    theta = walker_thetas(name, W, seed).T.copy()
+    sets = [v for k, v in STIFF_SETS.items() if k != "nonstiff"]
+    for j, w in enumerate(stiff_lanes):
+        theta[:, w] = sets[j % len(sets)][:theta.shape[0]]
+    return theta
+
+
+def _run(m, theta, trajectory=True):
+    W = theta.shape[1]
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    out = m.engine().integrate(y0, theta, trajectory=trajectory)
+    return y0, {k: (v.cpu().numpy() if v is not None else None) for k, v in out.items()}
+
+
+def _radau(ode, y0, times, th):
+    sol = solve_ivp(lambda t, y: ode(y, t, th), (times[0], times[-1]), y0, method="Radau", t_eval=times,
+                    rtol=1e-13, atol=1e-10)
+    assert sol.success
+    return sol.y.T
+
+
+@pytest.mark.parametrize("method", ["auto", "rosenbrock"])
+@pytest.mark.parametrize("W,stiff", [(1, [0]), (70, [3, 64, 69]), (200, [0, 1, 2, 130, 199])])
+def test_stiff_methods_bitwise_vs_c_restatement(method, W, stiff):
+    m = product_model("two_i", method=method)
+    theta = _mixed_thetas("two_i", W, stiff)
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"], equal_nan=True)
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
+    np.testing.assert_allclose(out["ssres"], ref["ssres"], rtol=1e-12)
+    assert np.array_equal(out["status"], ref["status"])
+    if method == "auto":
+        assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == sorted(stiff)
+    assert not (out["status"] & 4).any()
+
+
+@pytest.mark.parametrize("name", ["zero_i", "one_i"])
+def test_rosenbrock_other_models_bitwise(name):
+    m = product_model(name, method="rosenbrock")
+    theta = walker_thetas(name, 66).T.copy()
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"])
+    assert np.array_equal(out["status"], ref["status"])
+
+
+@pytest.mark.parametrize("method", ["auto", "rosenbrock"])
+def test_stiff_walkers_vs_tight_implicit_solution(method):
+    m = product_model("two_i", method=method)
+    W = 64
+    lanes = [5, 21, 40]
+    theta = _mixed_thetas("two_i", W, lanes)
+    y0, out = _run(m, theta)
+    for w in lanes + [0, 63]:
+        ref = _radau(CONFIGS["two_i"]["ode"], y0[:, w], m.times, theta[:, w])
+        np.testing.assert_allclose(out["traj"][:, :, w], ref, rtol=1e-6, atol=1e-6, err_msg=str(w))
+
+
+def test_auto_is_dopri5_without_stiff_walkers_at_c2_size():
+    """65 536 demo draws: nothing is evicted, so 'auto' gives DOPRI5's bits."""
+    W = 65536
+    theta = walker_thetas("two_i", W, seed=3).T.copy()
+    a = product_model("two_i", method="dopri5")
+    b = product_model("two_i", method="auto")
+    _, ra = _run(a, theta)
+    _, rb = _run(b, theta)
+    for k in ("traj", "chi", "ssres", "status"):
+        assert np.array_equal(ra[k], rb[k]), k
+
+
+def test_auto_chi_only_mode_equals_trajectory_mode():
+    """MCMC mode (no trajectory) and trajectory mode step identically (steps end on every
+    grid time either way), so the fused chi agrees bitwise."""
+    m = product_model("two_i", method="auto")
+    theta = _mixed_thetas("two_i", 130, [7, 100])
+    _, a = _run(m, theta, trajectory=True)
+    _, b = _run(m, theta, trajectory=False)
+    for k in ("chi", "ssres", "status"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("method", ["auto", "rosenbrock"])
+def test_mh_stiff_methods_vs_c_restatement(method):
+    """Philox MH chains where some proposals are stiff: the device chain equals the C
+    restatement's (rtol 1e-8 as for DOPRI5 MH: ocml vs libm exp/log in the proposal)."""
+    W = 128
+    m = product_model("two_i", method=method)
+    theta = _mixed_thetas("two_i", W, [1, 64, 65, 127])
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    walk = np.ones(5, np.uint8)
+    dev = m.engine().mh_run(theta, y0, nits=12, burnin=4, walk_mask=walk, rng="philox", seed=11)
+    ref = rk_ref.mh_run(m.fit_problem(), theta, y0, 12, 4, walk, rng="philox", seed=11)
+    np.testing.assert_allclose(dev["samples"].cpu().numpy(), ref["samples"], rtol=1e-8)
+
+
+def test_rtc_templated_body_gets_stiff_methods_bitwise():
+    """A user C body written over the scalar type R compiles for dual numbers: the RTC
+    module has the stiff methods and reproduces the built-in kernels bitwise."""
+    theta = _mixed_thetas("two_i", 96, [2, 50])
+    a = product_model("two_i", method="auto")
+    b = product_model("two_i", method="auto", device_rhs=TWO_I_TEMPLATED_BODY)
+    _, ra = _run(a, theta)
+    _, rb = _run(b, theta)
+    for k in ("traj", "chi", "ssres", "status"):
+        assert np.array_equal(ra[k], rb[k], equal_nan=True), k
+
+
+def test_rtc_double_only_body_reports_no_stiff_methods():
+    """A body with `double` temporaries has no dual-number Jacobian: RK4/DOPRI5 work,
+    the stiff methods are refused with OE_ERR_UNSUPPORTED (never silently replaced)."""
+    from test_gpu_rtc import ONE_I_FMA_BODY
+    m = product_model("one_i", method="dopri5", device_rhs=ONE_I_FMA_BODY)
+    _run(m, walker_thetas("one_i", 8).T.copy())
+    m2 = product_model("one_i", method="auto", device_rhs=ONE_I_FMA_BODY)
+    with pytest.raises(Exception, match="dual numbers"):
+        _run(m2, walker_thetas("one_i", 8).T.copy())
+
+
+def test_transpiled_time_forced_model_with_stiff_methods():
+    """A transpiled non-built-in model with a time forcing (∂f/∂t from the dual t):
+    'rosenbrock' and 'auto' within tolerance of the tight implicit solution."""
+    from odelib_amd import ModelFramework, parameter
+    df = demo_df({"virus": "V", "host": "S"})
+    th = {"mu": 0.5, "phi": 2e-7, "beta": 20.0, "delta": 0.3}
+    W = 70
+    theta = np.array(list(th.values()))[:, None] * np.exp(0.05 * np.random.RandomState(4).standard_normal((4, W)))
+    theta[3, 9] = 1e5  # a stiff virus decay in one lane
+    for method in ("rosenbrock", "auto"):
+        m = ModelFramework(ODE=sat_infection, parameter_names=list(th), state_names=["S", "V"], dataframe=df,
+                           method=method, **{k: parameter(init_value=v) for k, v in th.items()})
+        y0, out = _run(m, theta)
+        for w in (0, 9, 69):
+            ref = _radau(sat_infection, y0[:, w], m.times, theta[:, w])
+            np.testing.assert_allclose(out["traj"][:, :, w], ref, rtol=1e-6, atol=1e-6, err_msg=f"{method} {w}")
