@@ -6,8 +6,9 @@ Same constructor, attribute names, data set-up and method signatures as the refe
 and likelihood evaluation goes through ``libodelib_amd.so`` (``engine.Engine``).  The
 ODE callable is bound to a compiled device RHS by ``models.resolve``.
 
-Engine options (keyword-only, new): ``method`` ('dopri5' default — adaptive like
-odeint — or 'rk4'), ``rtol``/``atol`` (odeint defaults), ``rk4_substeps``,
+Engine options (keyword-only, new): ``method`` ('auto' default — like odeint's LSODA:
+adaptive DOPRI5 with a per-walker stiffness test, stiff walkers redone by an L-stable
+Rosenbrock method; 'dopri5' where that is unavailable — or 'dopri5', 'rosenbrock', 'rk4'), ``rtol``/``atol`` (odeint defaults), ``rk4_substeps``,
 ``max_steps`` (odeint's mxstep), ``device`` (HIP device index; default: torch's current
 device when the engine is built), ``device_model``
 (force a built-in RHS, or 'rtc'), ``device_rhs`` (C++ body of the RHS for hipRTC).
@@ -119,7 +120,10 @@ class ModelFramework:
         # engine options are keyword-only and never shadow a parameter / state name
         eng = {k: kwargs.pop(k) for k in list(kwargs) if k in _ENGINE_KW
                and k not in self._pnames and k not in self._snames}
-        self.method = eng.get("method", "dopri5")
+        # default 'auto': odeint's LSODA behaviour (non-stiff DOPRI5, stiff walkers by the
+        # Rosenbrock method); 'dopri5' where the stiff methods are unavailable
+        self.method = eng.get("method", "auto")
+        self._method_default = "method" not in eng
         self.rtol = float(eng.get("rtol", ODEINT_TOL))
         self.atol = float(eng.get("atol", ODEINT_TOL))
         self.rk4_substeps = int(eng.get("rk4_substeps", 1))
@@ -367,7 +371,8 @@ class ModelFramework:
                           obs_logsigma=cat(Ssig, float), obs_lin=cat(lin, float),
                           sstot=float(sstot) if cols else 1.0, pnum=int(self._pnum), method=self.method,
                           rk4_substeps=self.rk4_substeps, rtol=self.rtol, atol=self.atol,
-                          max_steps=self.max_steps, custom_source=dm.source)
+                          max_steps=self.max_steps, custom_source=dm.source,
+                          auto_fallback=bool(getattr(self, "_method_default", False)))
 
     def _problem_key(self, device):
         """What the uploaded FitProblem depends on.  It is recorded on the Engine itself

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("ODELIB_AMD_LIB", os.path.join(_HERE, "csrc", "libodel
 # --- constants mirrored from include/odelib_amd.h -----------------------------------
 OE_ABI_VERSION = 3
 OE_OK = 0
+OE_ERR_ARG, OE_ERR_HIP, OE_ERR_STATE, OE_ERR_UNSUPPORTED, OE_ERR_NOMEM = -1, -2, -3, -4, -5
 OE_METHOD_RK4, OE_METHOD_DOPRI5, OE_METHOD_AUTO, OE_METHOD_ROSENBROCK = 0, 1, 2, 3
 OE_MODEL_ZERO_I, OE_MODEL_ONE_I, OE_MODEL_TWO_I, OE_MODEL_CHAIN = 0, 1, 2, 3
 OE_MODEL_CUSTOM = 1000
@@ -41,6 +42,11 @@ EXPORTED = (
     "oe_numpy_streams",
     "oe_last_kernel_ms",
 )
+
+
+class NativeUnsupported(RuntimeError):
+    """OE_ERR_UNSUPPORTED: the model / method combination is not available (e.g. a stiff
+    method for n_states > 8, or for a C body that does not compile for dual numbers)."""
 
 
 class NativeUnavailable(RuntimeError):
@@ -188,7 +194,8 @@ class Context:
 
     def _check(self, rc: int, what: str):
         if rc != OE_OK:
-            raise RuntimeError(f"{what} failed ({rc}): {self.lib.oe_last_error(self._h).decode()}")
+            cls = NativeUnsupported if rc == OE_ERR_UNSUPPORTED else RuntimeError
+            raise cls(f"{what} failed ({rc}): {self.lib.oe_last_error(self._h).decode()}")
 
     def set_stream(self, stream_handle: int):
         """Launch on this hipStream_t handle (0 = the null stream)."""

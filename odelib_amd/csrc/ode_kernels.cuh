@@ -61,6 +61,7 @@ enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8
 // the Rosenbrock fallback for stiff / over-budget walkers (LSODA-like), Rosenbrock only
 enum : int { kRK4 = 0, kDOPRI5 = 1, kAuto = 2, kRos4 = 3 };
 constexpr int kStiffMaxS = 8;  // the stiff methods factor an S x S matrix per lane in registers
+constexpr int kStiffTestSteps = 3;  // auto: stiffness test from the 3rd step within one output interval
 
 // per-lane accumulators of the fused likelihood
 struct Acc {
@@ -513,9 +514,12 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
     ++nst;
 
     if (err <= 1.0) {
-      if constexpr (AUTO) {
-        // stiffness: h²·Σ(k7−k6)² > 3.25²·Σ(ynew − y6)² (y6 = the stage-6 input), i.e.
-        // h·|λ| > 3.25 (Hairer & Wanner I, §II.10); exact products, no square root
+      // stiffness: h²·Σ(k7−k6)² > 3.25²·Σ(ynew − y6)² (y6 = the stage-6 input), i.e.
+      // h·|λ| > 3.25 (Hairer & Wanner I, §II.10); exact products, no square root.  Tested
+      // only on steps that stay within one output interval for the 3rd time or more (a
+      // wave-uniform gate): a stiff lane pins the shared step far below the grid spacing,
+      // while a non-stiff wave spans grid points with nearly every step and never pays.
+      if (AUTO && nst >= kStiffTestSteps) {
         double stnum = 0.0, stden = 0.0;
 #pragma unroll
         for (int s = 0; s < S; ++s) {

@@ -46,6 +46,9 @@ class FitProblem:
     atol: float = ODEINT_TOL
     max_steps: int = 500
     custom_source: str | None = None        # user RHS body for hipRTC (model_id ignored)
+    auto_fallback: bool = False             # method 'auto' was a default: use 'dopri5' where
+                                            # the stiff methods are unavailable (S > 8, C body
+                                            # without a dual-number instantiation)
 
     def __post_init__(self):
         self.times = np.ascontiguousarray(self.times, dtype=np.float64)
@@ -190,7 +193,14 @@ class Engine:
         c = problem.to_c()
         if problem.custom_source is not None:  # compiled once per context (cached by source)
             c.model_id = self.ctx.model_compile(problem.custom_source, problem.n_states, problem.n_params)
-        self.ctx.problem_set(c)
+        try:
+            self.ctx.problem_set(c)
+        except N.NativeUnsupported:
+            if not (problem.method == "auto" and problem.auto_fallback):
+                raise
+            problem.method = "dopri5"
+            c.method = METHODS["dopri5"]
+            self.ctx.problem_set(c)
         self.problem = problem
         self.key = key
 

@@ -306,7 +306,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     double err = grp_max(L, nl, 1);
     ++nst;
     if (err <= 1.0) {
-      if (autom) {
+      if (autom && nst >= 3) { /* ode_kernels.cuh kStiffTestSteps */
         for (int l = 0; l < nl; ++l) {
           Lane* q = &L[l];
           double stnum = 0.0, stden = 0.0;
@@ -570,11 +570,12 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
     q->dead = !q->part;
     q->kobs = 0;
     if (q->part) emit(pb, 0, q->y, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
-    jac_eval(pb, q->y, t, p + l * MAXP, R[l].f0, R[l].J, R[l].ft);
+    if (q->part) jac_eval(pb, q->y, t, p + l * MAXP, R[l].f0, R[l].J, R[l].ft);
   }
   double h = INFINITY;
   for (int l = 0; l < nl; ++l) {
     Lane* q = &L[l];
+    if (q->dead) { h = fmin(h, tend - t0); continue; } /* sits out: votes the whole span */
     double d0 = 0.0, d1v = 0.0;
     for (int s = 0; s < S; ++s) {
       double sk = atol + rtol * fabs(q->y[s]);
@@ -617,6 +618,8 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
       Lane* q = &L[l];
       RosLane* rl = &R[l];
       const double* pl = p + l * MAXP;
+      if (q->dead) { q->el = 0.0; continue; } /* bystanders and evicted lanes: no vote (the
+                                                  kernel computes them and discards the result) */
       double lu[MAXS * MAXS], dinv[MAXS];
       int piv[MAXS];
       for (int r = 0; r < S; ++r)
@@ -656,7 +659,7 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
     if (err <= 1.0) {
       const double tn = clip ? ti : t + h;
       for (int l = 0; l < nl; ++l)
-        if (L[l].part) memcpy(L[l].y, R[l].y1, sizeof(double) * S);
+        if (L[l].part && !L[l].dead) memcpy(L[l].y, R[l].y1, sizeof(double) * S); /* evicted: stays NaN */
       t = tn;
       if (clip) {
         for (int l = 0; l < nl; ++l)
@@ -665,7 +668,8 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
         nst = 0;
       }
       if (i < pb->T)
-        for (int l = 0; l < nl; ++l) jac_eval(pb, L[l].y, t, p + l * MAXP, R[l].f0, R[l].J, R[l].ft);
+        for (int l = 0; l < nl; ++l)
+          if (!L[l].dead) jac_eval(pb, L[l].y, t, p + l * MAXP, R[l].f0, R[l].J, R[l].ft);
       double fac = (err > 0.0) ? 0.9 * inv_fourth_root(err) : 6.0;
       fac = fmin(6.0, fmax(0.2, fac));
       if (last_rej) fac = fmin(fac, 1.0);
