@@ -339,26 +339,44 @@ def main():
         extra = {}
         # C4's per-GPU shard: 1 048 576 walkers over 8 GPUs = 131 072 per GPU (the N=8 run of
         # this bench is weak-scaled at the metric's 65 536 walkers per GPU)
-        for name, model, method, W in (("C2", "two_i", "dopri5", 65536), ("C3", "chain20", "rk4", 262144),
-                                       ("C3-dopri5", "chain20", "dopri5", 262144),
-                                       ("C4-shard", "two_i", "rk4", 131072)):
+        # C2-stiffmix: the C2 draws with 0.1 % of the walkers made stiff (tau = 1e5, the
+        # I1 compartment relaxing 4e4x faster): 'dopri5' keeps them in the shared step, so
+        # their waves crawl at the stability limit; 'auto' (the drop-in default, LSODA-like)
+        # hands them to the Rosenbrock method
+        for name, model, method, W, stiff in (("C2", "two_i", "dopri5", 65536, 0.0),
+                                              ("C2-auto", "two_i", "auto", 65536, 0.0),
+                                              ("C2-stiffmix-dopri5", "two_i", "dopri5", 65536, 1e-3),
+                                              ("C2-stiffmix-auto", "two_i", "auto", 65536, 1e-3),
+                                              ("C3", "chain20", "rk4", 262144, 0.0),
+                                              ("C3-dopri5", "chain20", "dopri5", 262144, 0.0),
+                                              ("C4-shard", "two_i", "rk4", 131072, 0.0)):
             mx, y0x = build_problem(model, method, T)
             mx.device = dev_index
             ex = mx.engine()
             Sx = len(y0x)
-            thx = torch.as_tensor(synthetic_walkers(W, P), device=dev).contiguous()
+            thh = synthetic_walkers(W, P)
+            n_stiff = int(round(stiff * W))
+            if n_stiff:
+                thh[4, np.random.RandomState(7).choice(W, n_stiff, replace=False)] = 1e5
+            thx = torch.as_tensor(thh, device=dev).contiguous()
             y0t = torch.as_tensor(np.repeat(y0x[:, None], W, axis=1), device=dev).contiguous()
             trx = ex.empty_traj(W)
             ms = []
-            for r in range(15):  # 5 untimed launches (clocks and caches settle), median of 10
-                ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True)
-                if r >= 5:
+            reps = 15 if not n_stiff else 6
+            for r in range(reps):  # untimed launches first (clocks and caches settle), then the median
+                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True)
+                if r >= reps // 3:
                     ms.append(ex.last_kernel_ms())
             kms = float(np.median(ms))
             byt = W * (T - 1) * 8 * Sx
-            extra[name] = {"workload": f"{model} {method}, {W} walkers, trajectory mode", "kernel_ms": kms,
+            extra[name] = {"workload": f"{model} {method}, {W} walkers, trajectory mode"
+                           + (f", {n_stiff} stiff walkers (tau=1e5)" if n_stiff else ""), "kernel_ms": kms,
                            "walker_timesteps_per_s": W * (T - 1) / (kms / 1e3),
                            "hbm_frac": byt / (kms / 1e3) / 1e9 / HBM_PEAK_GBS}
+            if n_stiff:
+                stx = outx["status"].cpu().numpy()
+                extra[name]["walkers_flagged_stiff"] = int(((stx & 8) != 0).sum())
+                extra[name]["walkers_maxstep"] = int(((stx & 4) != 0).sum())
             del trx, thx, y0t, ex
             torch.cuda.empty_cache()
 
