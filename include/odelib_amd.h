@@ -88,16 +88,18 @@ enum {
   OE_HOST_PTRS = 1u, /* buffers are host memory */
   OE_ASYNC = 2u,     /* do not synchronize before returning (device pointers only) */
   OE_NT_STORES = 4u, /* non-temporal trajectory stores */
-  OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel (opt-in, S <= 8, W even) */
+  OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel, 2 store waves (S <= 8, W even) */
   OE_HALF_WAVES = 16u, /* RK4: 32 walkers per wavefront (twice the waves; same results). Chosen
                          automatically for trajectories with S >= 5 at <= 1 wave per SIMD. */
   /* 32u: reserved (was an experimental split-wave layout, measured slower and removed) */
   OE_NO_XCD_REMAP = 64u, /* oe_integrate: keep blockIdx-order walker blocks.  By default the
                            blocks an XCD receives (round-robin dispatch) take one contiguous
                            range of walkers (same results, faster trajectory stores) */
-  OE_NO_TIMING = 128u   /* oe_integrate: record no timing events around the launch (back-to-back
+  OE_NO_TIMING = 128u,  /* oe_integrate: record no timing events around the launch (back-to-back
                            launches without event markers between them); oe_last_kernel_ms
                            then reports OE_ERR_STATE until a timed call */
+  OE_PIPE_4 = 512u,     /* as OE_PIPE with 4 / 8 store waves per 4 compute waves (opt-in) */
+  OE_PIPE_8 = 1024u
 };
 
 /* RNG modes for oe_mh_run */

@@ -469,16 +469,24 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     ia.y0 = y0; ia.theta = theta; ia.traj = traj; ia.chi = chi; ia.ssres = ssres; ia.status = status;
   }
 
-  // opt-in producer/consumer RK4 trajectory kernel (16-B stores from dedicated store
-  // waves; needs W even).  Measured 0.433 vs 0.420 ms for the direct kernel on C1, so
-  // it is not the default.
-  const bool piped = (flags & OE_PIPE) && !e->rtc && c->method == OE_METHOD_RK4 && ia.traj && e->rk4_piped[nt ? 1 : 0] &&
-                     (W % 2 == 0);
+  // Opt-in producer/consumer RK4 trajectory kernel (4 compute waves hand each row to 2, 4
+  // or 8 dedicated store waves through a 128 KiB LDS ring; 16-B stores; needs W even).
+  // Isolated launches run faster than the direct kernel (C1 0.365 vs 0.396 ms: part of
+  // the 2.1 GB stays dirty in the 256 MB MALL when the launch ends), back-to-back
+  // launches — the bench — do not (0.3995 vs 0.3912 ms): both then sit at the sustained
+  // store rate of the chip, so it is not the default.
+  int pipe_v = -1;
+  if (flags & OE_PIPE_8) pipe_v = 2;
+  else if (flags & OE_PIPE_4) pipe_v = 1;
+  else if (flags & OE_PIPE) pipe_v = 0;
+  const bool piped = pipe_v >= 0 && !e->rtc && c->method == OE_METHOD_RK4 && ia.traj && (W % 2 == 0) &&
+                     e->rk4_piped[pipe_v][nt ? 1 : 0];
+  ia.xcd_remap = (flags & OE_NO_XCD_REMAP) ? 0 : 1;
   const bool timing = !(flags & OE_NO_TIMING);
   if (timing) OE_HIP(c, hipEventRecord(c->ev0, c->stream));
   if (piped) {
-    const dim3 grid((unsigned)((W + kPipeWalkers - 1) / kPipeWalkers)), block(kPipeThreads);
-    e->rk4_piped[nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
+    const dim3 grid((unsigned)((W + kPipeWalkers - 1) / kPipeWalkers)), block(256 + 64 * (2 << pipe_v));
+    e->rk4_piped[pipe_v][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
   } else {
     // RK4 trajectories of 5+ states at <= 1 wave per SIMD are store-issue bound: run
     // 32 walkers per wave (twice the storing waves; same bits).  Measured on MI355X at
@@ -490,7 +498,6 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     ia.half = (rk4 && ((flags & OE_HALF_WAVES) || auto_half)) ? 1 : 0;
     const int64_t per_block = ia.half ? kBlock / 2 : kBlock;
     const dim3 grid((unsigned)((W + per_block - 1) / per_block)), block(kBlock);
-    ia.xcd_remap = (flags & OE_NO_XCD_REMAP) ? 0 : 1;
     OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));
   }
   OE_HIP(c, hipGetLastError());

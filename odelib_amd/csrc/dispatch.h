@@ -18,7 +18,7 @@ struct Entry {
   int32_t P;  // the model's own parameter count
   // [method][traj][nt]; methods kAuto / kRos4 are null when S > kStiffMaxS
   IntegrateLaunch integrate[4][2][2];
-  IntegrateLaunch rk4_piped[2];  // [nt]; null when S > 8 (LDS ring too large)
+  IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > 8
   MHLaunch mh[4];
   const RtcModule* rtc = nullptr;  // user RHS compiled at run time (launchers above unused)
 };
@@ -51,9 +51,9 @@ template <class M, int METHOD, bool TRAJ, bool NT>
 void launch_integrate(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_integrate<M, METHOD, TRAJ, NT>), g, b, 0, s, pb, ia);
 }
-template <class M, bool NT>
+template <class M, bool NT, int NSW>
 void launch_rk4_piped(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
-  hipLaunchKernelGGL((k_integrate_rk4_piped<M, NT>), g, b, 0, s, pb, ia);
+  hipLaunchKernelGGL((k_integrate_rk4_piped<M, NT, NSW>), g, b, 0, s, pb, ia);
 }
 template <class M, int METHOD>
 void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
@@ -82,8 +82,12 @@ Entry make_entry(int32_t model_id) {
     fill_method<M, kRos4>(e);
   }
   if constexpr (M::S <= 8) {
-    e.rk4_piped[0] = launch_rk4_piped<M, false>;
-    e.rk4_piped[1] = launch_rk4_piped<M, true>;
+    e.rk4_piped[0][0] = launch_rk4_piped<M, false, 2>;
+    e.rk4_piped[0][1] = launch_rk4_piped<M, true, 2>;
+    e.rk4_piped[1][0] = launch_rk4_piped<M, false, 4>;
+    e.rk4_piped[1][1] = launch_rk4_piped<M, true, 4>;
+    e.rk4_piped[2][0] = launch_rk4_piped<M, false, 8>;
+    e.rk4_piped[2][1] = launch_rk4_piped<M, true, 8>;
   }
   return e;
 }

@@ -747,17 +747,17 @@ __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const In
 // ---------------------------------------------------------------------------------
 // Kernel 1b: RK4 trajectory mode with producer/consumer waves (S <= 8, W even).
 //
-// One 384-thread workgroup = 4 COMPUTE waves (256 walkers, one per lane) + 2 STORE
-// waves.  Output rows are produced in phases of H rows into one half of a
+// One workgroup = 4 COMPUTE waves (256 walkers, one per lane) + NSW STORE waves (2, 4
+// or 8).  Output rows are produced in phases of H rows into one half of a
 // double-buffered LDS ring [2][H][S][256]; in the next phase the store waves read that
 // half with ds_read_b128 (two consecutive walkers per lane) and write 1 KB per
 // wave-instruction with buffer_store_dwordx4, while the compute waves fill the other
-// half.  Phases are separated by a raw s_barrier behind an lgkmcnt(0) wait only, so
+// half.  Store wave j covers walker half j & 1 and the states s ≡ j/2 (mod NSW/2).
+// Phases are separated by a raw s_barrier behind an lgkmcnt(0) wait only, so
 // the global stores stay in flight across barriers and the compute waves never wait on
 // vmcnt.  Same arithmetic, same outputs as k_integrate<M, RK4, true, NT>.
 // ---------------------------------------------------------------------------------
 constexpr int kPipeWalkers = 256;  // walkers per workgroup (4 compute waves)
-constexpr int kPipeThreads = 384;  // + 2 store waves
 constexpr int kPipeLdsBytes = 128 * 1024;
 
 template <int S>
@@ -770,18 +770,21 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 
-template <class M, bool NT>
-__global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevProblem pb, const IntegrateArgs ia) {
+template <class M, bool NT, int NSW>
+__global__ void __launch_bounds__(256 + 64 * NSW) k_integrate_rk4_piped(const DevProblem pb, const IntegrateArgs ia) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
   constexpr int H = pipe_rows<S>();
   static_assert(2 * H * S * kPipeWalkers * 8 <= kPipeLdsBytes, "LDS ring too large");
-  __shared__ double ring[2][H][S][kPipeWalkers];
+  __shared__ double pipe_ring[2][H][S][kPipeWalkers];
+  auto ring = [&](int half, int h, int s, int b) -> double* { return &pipe_ring[half][h][s][b]; };
 
   const int64_t W = ia.W;
   const int T = pb.T;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
+  // blockIdx order (the XCD-contiguous remap of the direct kernel measured 9 % slower here:
+  // 0.400 vs 0.366 ms on C1, profiles/r02l_time_modes.log)
   const int64_t base = (int64_t)blockIdx.x * kPipeWalkers;
   const int nphase = (T + H - 1) / H;
 
@@ -803,7 +806,7 @@ __global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevP
     const int n = pb.substeps;
     auto put = [&](int half, int h, const double (&v)[S]) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) ring[half][h][s][b] = v[s];
+      for (int s = 0; s < S; ++s) *ring(half, h, s, b) = v[s];
 #pragma unroll
       for (int s = 0; s < S; ++s) a.ymin = min_raw(a.ymin, v[s]);
     };
@@ -848,8 +851,10 @@ __global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevP
     }
   } else {
     // ------------------------------ store waves --------------------------------
-    const int sw = wave - 4;                 // 0 or 1: walkers [128*sw, 128*sw + 128)
-    const int b = sw * 128 + 2 * lane;       // first of this lane's two walkers
+    const int sw = wave - 4;                 // store wave 0 .. NSW-1
+    constexpr int G = NSW / 2;               // state groups
+    const int sg = sw >> 1;                  // this wave's states: sg, sg + G, ...
+    const int b = (sw & 1) * 128 + 2 * lane; // first of this lane's two walkers
     const bool active = base + b < W;        // W even: both or neither
     const uint32_t off = (uint32_t)(base + b) * 8u;
     const uint32_t row_bytes = (uint32_t)(S * W * 8);
@@ -862,8 +867,10 @@ __global__ void __launch_bounds__(kPipeThreads) k_integrate_rk4_piped(const DevP
           const __amdgpu_buffer_rsrc_t rsrc =
               __builtin_amdgcn_make_buffer_rsrc((void*)(ia.traj + (int64_t)r * S * W), 0, row_bytes, 0x00020000);
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            const u32x4 v = *reinterpret_cast<const u32x4*>(&ring[half][r - r0][s][b]);
+          for (int s0 = 0; s0 < S; s0 += G) {
+            const int s = s0 + sg;
+            if (G > 1 && s >= S) break;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(ring(half, r - r0, s, b));
             if (active)
               __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, (uint32_t)(s * W * 8), NT ? 2 : 0);
           }

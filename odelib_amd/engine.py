@@ -228,12 +228,12 @@ class Engine:
 
     # -- batched integrate -------------------------------------------------------------------
     def integrate(self, y0, theta, trajectory: bool = True, traj_out=None, nt_stores: bool = True,
-                  sync: bool = True, pipelined: bool = False, half_waves: bool = False,
+                  sync: bool = True, pipelined=None, half_waves: bool = False,
                   xcd_remap: bool = True, timing: bool = True):
         """y0 [S][W], theta [P][W] → dict(traj [T][S][W] | None, chi [W], ssres [W], status [W]).
 
-        ``pipelined=True`` selects the opt-in producer/consumer RK4 trajectory kernel
-        (same results; not faster on MI355X).  ``half_waves=True`` runs
+        ``pipelined=True`` (or 2, 4, 8: store waves per 4 compute waves) selects the
+        opt-in producer/consumer RK4 trajectory kernel (same results).  ``half_waves=True`` runs
         32 walkers per wavefront (twice the waves; same results).
         ``xcd_remap=False`` keeps blockIdx-order walker blocks instead of one contiguous
         walker range per XCD (same results).  ``timing=False`` records no library events
@@ -254,7 +254,8 @@ class Engine:
         ssres = torch.empty(W, dtype=torch.float64, device=self.dev)
         status = torch.empty(W, dtype=torch.int32, device=self.dev)
         self._sync_stream()
-        flags = N.OE_ASYNC | (N.OE_NT_STORES if nt_stores else 0) | (N.OE_PIPE if pipelined else 0) \
+        pipe = {None: 0, False: 0, True: N.OE_PIPE, 2: N.OE_PIPE, 4: N.OE_PIPE_4, 8: N.OE_PIPE_8}[pipelined]
+        flags = N.OE_ASYNC | (N.OE_NT_STORES if nt_stores else 0) | pipe \
             | (N.OE_HALF_WAVES if half_waves else 0) \
             | (0 if xcd_remap else N.OE_NO_XCD_REMAP) | (0 if timing else N.OE_NO_TIMING)
         self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)

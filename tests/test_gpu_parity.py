@@ -71,10 +71,11 @@ def test_rk4_pipelined_kernel_matches_direct_kernel(spec, W):
     theta = _walkers(spec, W)
     y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
     eng = m.engine()
-    a = eng.integrate(y0, theta, pipelined=True)
     b = eng.integrate(y0, theta, pipelined=False)
-    for key in ("traj", "chi", "ssres", "status"):
-        assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
+    for nsw in (2, 4, 8):  # store waves per 4 compute waves
+        a = eng.integrate(y0, theta, pipelined=nsw)
+        for key in ("traj", "chi", "ssres", "status"):
+            assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), (nsw, key)
     for nt in (False, True):
         c = eng.integrate(y0, theta, pipelined=True, nt_stores=nt)
         assert np.array_equal(c["traj"].cpu().numpy(), b["traj"].cpu().numpy())

@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--cases", nargs="+", default=["two_i:rk4:65536", "two_i:dopri5:65536"])
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--modes", nargs="+", default=["traj", "notraj", "traj_half", "traj_noxcd"],
-                    help="traj/notraj + optional _half, _noxcd, _stab (scalar-load step table)")
+                    help="traj/notraj + optional _half, _noxcd, _pipe / _pipe4 / _pipe8 (producer/consumer store waves), _auto (library choice; default: direct kernel)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -41,7 +41,8 @@ def main():
                 eng.integrate(y0, theta, trajectory=mode.startswith("traj"),
                               traj_out=traj if mode.startswith("traj") else None, sync=True,
                               half_waves="half" in mode, xcd_remap="noxcd" not in mode,
-                              lds_table="stab" not in mode)
+                              pipelined=(8 if "pipe8" in mode else 4 if "pipe4" in mode else 2 if "pipe" in mode
+                                         else None if "auto" in mode else False))
                 if r >= 3:
                     ms[mode].append(eng.last_kernel_ms())
         for mode in modes:
