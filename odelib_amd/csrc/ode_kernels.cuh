@@ -1031,8 +1031,15 @@ __device__ __forceinline__ T* opaque(T* p) {
   return p;
 }
 
+// The stiff methods' Rosenbrock fallback (dual-number Jacobian, in-register LU) would set
+// the register budget of the whole MH kernel (chain5 'auto': 300 VGPR+AGPR, one wave per
+// SIMD, +49 % per iteration at 262 144 walkers); for S = 5, where the plain DOPRI5 MH
+// kernel runs two waves per SIMD, asking for two keeps the DOPRI5 phase there (80 B of
+// scratch, in the rare path).  S = 6..8 DOPRI5 MH kernels are at one wave per SIMD anyway.
 template <class M, int METHOD>
-__global__ void __launch_bounds__(256) k_mh(const DevProblem pb, const MHArgs ma) {
+__global__ void __launch_bounds__(256)
+    __attribute__((amdgpu_waves_per_eu((METHOD >= kAuto && M::S == 5) ? 2 : 1)))
+    k_mh(const DevProblem pb, const MHArgs ma) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
   const int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
