@@ -228,6 +228,39 @@ def test_full_size_c1_bitwise_and_properties():
     np.testing.assert_allclose(out["traj"], dp["traj"], rtol=1e-6, atol=1e-6)
 
 
+def test_full_size_c2_dopri5_bitwise():
+    """BASELINE configs[2]: two_i, 65 536 walkers, DOPRI5 with the wavefront error norm at
+    odeint's tolerances — bitwise against the C restatement (64-walker lockstep groups)
+    over the whole ensemble."""
+    W = 65536
+    m = _model("two_i", "dopri5")
+    rs = np.random.RandomState(2)
+    theta = np.asarray([THETA["two_i"][p] for p in CONFIGS["two_i"]["pnames"]])[:, None] * \
+        np.exp(0.05 * rs.standard_normal((5, W)))
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta, trajectory=True)
+    assert np.array_equal(out["traj"], ref["traj"])
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
+    assert np.array_equal(out["status"], ref["status"]) and (out["status"] == 0).all()
+
+
+def test_c3_chain20_dopri5_groups_bitwise():
+    """configs[3] with DOPRI5: 20-state chain, 262 144 walkers; three whole lockstep groups
+    (64 consecutive walkers share the step size) against the C restatement, bitwise."""
+    W = 262144
+    m = _model("chain20", "dopri5")
+    rs = np.random.RandomState(3)
+    theta = np.asarray(list(THETA["two_i"].values()))[:, None] * np.exp(0.05 * rs.standard_normal((5, W)))
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    out = m.engine().integrate(y0, theta, trajectory=True)
+    for g in (0, 2049, W // 64 - 1):
+        sl = slice(64 * g, 64 * g + 64)
+        ref = rk_ref.integrate(m.fit_problem(), y0[:, sl].copy(), theta[:, sl].copy())
+        assert np.array_equal(out["traj"][:, :, sl].cpu().numpy(), ref["traj"]), g
+        np.testing.assert_allclose(out["chi"][sl].cpu().numpy(), ref["chi"], rtol=1e-12)
+    del out
+
+
 def test_c3_chain20_size_properties():
     """configs[3] size: 20-state chain, 262 144 walkers (42 GB trajectory in HBM)."""
     W = 262144
