@@ -43,6 +43,42 @@ __global__ void __launch_bounds__(256) k_store(double* out, int W, int T) {
   }
 }
 
+// linear fill of the same bytes: 16 B per lane, consecutive lanes consecutive addresses,
+// grid-stride — the chip's streaming-write ceiling for comparison.  MODE 0: NT stores of
+// non-zero data; 1: plain stores of non-zero data; 2: plain stores of zeros; 3: NT zeros
+template <int MODE>
+__global__ void __launch_bounds__(256) k_fill(double* out, long n2) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  d2v* p = reinterpret_cast<d2v*>(out);
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+    d2v v = (MODE >= 2) ? d2v{0.0, 0.0} : d2v{1.0 + i, 2.0};
+    if (MODE == 0 || MODE == 3) __builtin_nontemporal_store(v, p + i);
+    else p[i] = v;
+  }
+}
+
+template <class F>
+float median_ms(F launch) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  std::vector<float> ms;
+  for (int r = 0; r < 13; ++r) {  // back to back, one event pair per launch
+    CHECK(hipEventRecord(a));
+    launch();
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float x;
+    CHECK(hipEventElapsedTime(&x, a, b));
+    if (r >= 3) ms.push_back(x);
+  }
+  std::sort(ms.begin(), ms.end());
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+  return ms[ms.size() / 2];
+}
+
 template <int SPLIT>
 void run(double* out, int W, int T) {
   const int threads = W * SPLIT;
@@ -77,6 +113,23 @@ int main() {
     run<1>(out, W, T);
     run<2>(out, W, T);
     run<4>(out, W, T);
+  }
+  const double bytes = (double)T * 4 * W * 8;
+  const long n2 = (long)T * 4 * W / 2;
+  for (int mode = 0; mode < 4; ++mode)
+    for (int blocks : {1024, 4096}) {
+      const float ms = median_ms([&] {
+        if (mode == 0) hipLaunchKernelGGL(k_fill<0>, dim3(blocks), dim3(256), 0, 0, out, n2);
+        if (mode == 1) hipLaunchKernelGGL(k_fill<1>, dim3(blocks), dim3(256), 0, 0, out, n2);
+        if (mode == 2) hipLaunchKernelGGL(k_fill<2>, dim3(blocks), dim3(256), 0, 0, out, n2);
+        if (mode == 3) hipLaunchKernelGGL(k_fill<3>, dim3(blocks), dim3(256), 0, 0, out, n2);
+      });
+      printf("{\"fill_mode\": %d, \"blocks\": %d, \"kernel_ms\": %.4f, \"TBps\": %.3f}\n", mode, blocks, ms,
+             bytes / (ms * 1e-3) / 1e12);
+    }
+  for (int byte : {0, 0x3F}) {
+    const float ms = median_ms([&] { CHECK(hipMemsetAsync(out, byte, (size_t)bytes, 0)); });
+    printf("{\"memset_byte\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n", byte, ms, bytes / (ms * 1e-3) / 1e12);
   }
   CHECK(hipFree(out));
   return 0;
