@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--method", default="rk4", choices=["rk4", "dopri5"])
     ap.add_argument("--times", type=int, default=1000)
     ap.add_argument("--cached-stores", action="store_true", help="plain (cached) trajectory stores")
+    ap.add_argument("--kernel", default="direct", choices=["direct", "pipe2", "pipe4", "pipe8"],
+                    help="RK4 trajectory kernel (A/B of the opt-in producer/consumer variants)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mcmc-iters", type=int, default=21, help="MCMC leg iterations (0 = skip)")
@@ -81,6 +83,9 @@ def pmc_traffic(args):
         return f["mean"] * 1024 * 2 + w["mean"] * 1024, f"rocprofv3 PMC FETCH_SIZE(x2)+WRITE_SIZE, {f['dispatches']} dispatches"
     except BaseException as e:  # never let profiling break the bench line
         return None, f"PMC pass failed: {e!r}"[:200]
+
+
+PIPE_ARG = {"direct": False, "pipe2": 2, "pipe4": 4, "pipe8": 8}
 
 
 def build_problem(model: str, method: str, T: int):
@@ -239,7 +244,7 @@ def main():
         # no timing-event markers between the timed launches (measured: markers between
         # back-to-back launches cost ~4 % of the C1 wall time, tools/launch_gaps.py)
         return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores,
-                             sync=False, timing=timing)
+                             sync=False, timing=timing, pipelined=PIPE_ARG[args.kernel])
 
     for _ in range(args.warmup):
         step()
@@ -389,7 +394,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"{args.model} {args.method} trajectory-mode integrate + fused chi",
                        "walkers_per_gpu": Wl, "walkers_total": Wl * n_gpus, "states": S, "times": T,
-                       "method": args.method, "stores": "cached" if args.cached_stores else "nontemporal", "parallelism": f"walker-shard x{n_gpus}"},
+                       "method": args.method, "stores": "cached" if args.cached_stores else "nontemporal",
+                       "kernel": args.kernel, "parallelism": f"walker-shard x{n_gpus}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_s * 1e3, "kernel_ms_note": "timed-region event span / steps",
