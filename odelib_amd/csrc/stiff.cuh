@@ -13,8 +13,9 @@
 //   * Jacobian: exact, by forward-mode dual numbers through the model's own templated
 //     RHS (built-in models and hipRTC user models alike): J = ∂f/∂y and ∂f/∂t in one
 //     evaluation with S + 1 tangents, value part bitwise equal to the plain RHS.
-//   * Linear algebra: (1/(γh) I − J) is factored per lane in registers (LU with partial
-//     pivoting; row swaps by selects, so nothing is indexed by a per-lane value).
+//   * Linear algebra: (1/(γh) I − J) is factored per lane in registers (LU with threshold
+//     partial pivoting; row swaps by selects, so nothing is indexed by a per-lane value,
+//     skipped by a wave none of whose lanes needs them).
 //   * Output: steps end on every grid time (no interpolation; stiff components make
 //     Hermite interpolation from f useless), so each row is a step endpoint.
 //   * Step control: max-norm error as DOPRI5, fac = 0.9·err^(−1/4) in [0.2, 6], wave
@@ -210,27 +211,45 @@ __device__ __forceinline__ double inv_fourth_root(double x) {
   return ldexp(c * y, -q);
 }
 
-// LU with partial pivoting (first maximum), full-row interchanges by selects.
+// LU with threshold partial pivoting: column k is pivoted only when |a_kk| < 0.1 x the
+// largest |a_ik| below it, and then on the first maximum (full-row interchanges by
+// selects).  (1/(γh))·I − J is nearly always diagonally dominant enough, so a wave skips
+// the interchange work of a column (and the solves skip theirs) unless one of its lanes
+// needs it: the selects cost ~40 % of a Rosenbrock step when done unconditionally.
+constexpr double kPivotThreshold = 0.1;
+
 template <int S>
-__device__ __forceinline__ void lu_factor(double (&a)[S][S], int (&piv)[S], double (&dinv)[S]) {
+__device__ __forceinline__ bool lu_factor(double (&a)[S][S], int (&piv)[S], double (&dinv)[S]) {
+  bool any_swap = false;  // wave-uniform: some lane interchanged rows
 #pragma unroll
   for (int k = 0; k < S; ++k) {
-    int pk = k;
-    double best = fabs(a[k][k]);
+    piv[k] = k;
+    if (k + 1 < S) {
+      double colmax = 0.0;
 #pragma unroll
-    for (int i = k + 1; i < S; ++i) {
-      const double v = fabs(a[i][k]);
-      if (v > best) { best = v; pk = i; }
-    }
-    piv[k] = pk;
+      for (int i = k + 1; i < S; ++i) colmax = fmax(colmax, fabs(a[i][k]));
+      const bool need = fabs(a[k][k]) < kPivotThreshold * colmax;
+      if (__ballot(need) != 0ull) {
+        any_swap = true;
+        int pk = k;
+        double best = fabs(a[k][k]);
 #pragma unroll
-    for (int i = k + 1; i < S; ++i) {
-      const bool sw = pk == i;
+        for (int i = k + 1; i < S; ++i) {
+          const double v = fabs(a[i][k]);
+          if (v > best) { best = v; pk = i; }
+        }
+        if (!need) pk = k;
+        piv[k] = pk;
 #pragma unroll
-      for (int j = 0; j < S; ++j) {
-        const double ak = a[k][j], ai = a[i][j];
-        a[k][j] = sw ? ai : ak;
-        a[i][j] = sw ? ak : ai;
+        for (int i = k + 1; i < S; ++i) {
+          const bool sw = pk == i;
+#pragma unroll
+          for (int j = 0; j < S; ++j) {
+            const double ak = a[k][j], ai = a[i][j];
+            a[k][j] = sw ? ai : ak;
+            a[i][j] = sw ? ak : ai;
+          }
+        }
       }
     }
     const double inv = 1.0 / a[k][k];
@@ -243,20 +262,24 @@ __device__ __forceinline__ void lu_factor(double (&a)[S][S], int (&piv)[S], doub
       for (int j = k + 1; j < S; ++j) a[i][j] = fma(-l, a[k][j], a[i][j]);
     }
   }
+  return any_swap;
 }
 
-// solve (LU) x = P b in place: all interchanges, then L (unit) forward, U backward
+// solve (LU) x = P b in place: all interchanges (skipped when no lane of the wave made
+// one), then L (unit) forward, U backward
 template <int S>
 __device__ __forceinline__ void lu_solve(const double (&a)[S][S], const int (&piv)[S], const double (&dinv)[S],
-                                         double (&b)[S]) {
+                                         bool any_swap, double (&b)[S]) {
+  if (any_swap) {
 #pragma unroll
-  for (int k = 0; k < S; ++k) {
+    for (int k = 0; k < S; ++k) {
 #pragma unroll
-    for (int i = k + 1; i < S; ++i) {
-      const bool sw = piv[k] == i;
-      const double bk = b[k], bi = b[i];
-      b[k] = sw ? bi : bk;
-      b[i] = sw ? bk : bi;
+      for (int i = k + 1; i < S; ++i) {
+        const bool sw = piv[k] == i;
+        const double bk = b[k], bi = b[i];
+        b[k] = sw ? bi : bk;
+        b[i] = sw ? bk : bi;
+      }
     }
   }
 #pragma unroll
@@ -344,26 +367,26 @@ __device__ __forceinline__ void integrate_ros4(const DevProblem& pb, double (&y)
     for (int r = 0; r < S; ++r)
 #pragma unroll
       for (int c = 0; c < S; ++c) lu[r][c] = (r == c) ? gh - J[r][c] : -J[r][c];
-    lu_factor<S>(lu, piv, dinv);
+    const bool any_swap = lu_factor<S>(lu, piv, dinv);
     double g1[S], g2[S], g3[S], g4[S], yt[S], fv[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) g1[s] = fma(hg1, ft[s], f0[s]);
-    lu_solve<S>(lu, piv, dinv, g1);
+    lu_solve<S>(lu, piv, dinv, any_swap, g1);
 #pragma unroll
     for (int s = 0; s < S; ++s) yt[s] = fma(a21, g1[s], y[s]);
     M::rhs(yt, t + a2x * h, p, fv);
 #pragma unroll
     for (int s = 0; s < S; ++s) g2[s] = fma(hg2, ft[s], fma(c21h, g1[s], fv[s]));
-    lu_solve<S>(lu, piv, dinv, g2);
+    lu_solve<S>(lu, piv, dinv, any_swap, g2);
 #pragma unroll
     for (int s = 0; s < S; ++s) yt[s] = fma(a32, g2[s], fma(a31, g1[s], y[s]));
     M::rhs(yt, t + a3x * h, p, fv);
 #pragma unroll
     for (int s = 0; s < S; ++s) g3[s] = fma(hg3, ft[s], fma(c32h, g2[s], fma(c31h, g1[s], fv[s])));
-    lu_solve<S>(lu, piv, dinv, g3);
+    lu_solve<S>(lu, piv, dinv, any_swap, g3);
 #pragma unroll
     for (int s = 0; s < S; ++s) g4[s] = fma(hg4, ft[s], fma(c43h, g3[s], fma(c42h, g2[s], fma(c41h, g1[s], fv[s]))));
-    lu_solve<S>(lu, piv, dinv, g4);
+    lu_solve<S>(lu, piv, dinv, any_swap, g4);
     double y1[S];
     double num = 0.0, den = 1.0, nfe = 0.0;
 #pragma unroll

@@ -519,14 +519,21 @@ static double inv_fourth_root(double x) {
 
 double ref_inv_fourth_root(double x) { return inv_fourth_root(x); }
 
-/* LU with partial pivoting (first maximum, full-row interchanges), a is S x S row-major */
+/* LU with threshold partial pivoting (stiff.cuh lu_factor): column k is pivoted only when
+   |a_kk| < 0.1 x max_{i>k} |a_ik|, then on the first maximum; a is S x S row-major */
 static void lu_factor(int S, double* a, int* piv, double* dinv) {
   for (int k = 0; k < S; ++k) {
     int pk = k;
-    double best = fabs(a[k * S + k]);
-    for (int i = k + 1; i < S; ++i) {
-      double v = fabs(a[i * S + k]);
-      if (v > best) { best = v; pk = i; }
+    if (k + 1 < S) {
+      double colmax = 0.0;
+      for (int i = k + 1; i < S; ++i) colmax = fmax(colmax, fabs(a[i * S + k]));
+      if (fabs(a[k * S + k]) < 0.1 * colmax) {
+        double best = fabs(a[k * S + k]);
+        for (int i = k + 1; i < S; ++i) {
+          double v = fabs(a[i * S + k]);
+          if (v > best) { best = v; pk = i; }
+        }
+      }
     }
     piv[k] = pk;
     if (pk != k)
