@@ -366,16 +366,28 @@ def main():
             thx = torch.as_tensor(thh, device=dev).contiguous()
             y0t = torch.as_tensor(np.repeat(y0x[:, None], W, axis=1), device=dev).contiguous()
             trx = ex.empty_traj(W)
-            ms = []
-            reps = 15 if not n_stiff else 6
-            for r in range(reps):  # untimed launches first (clocks and caches settle), then the median
-                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True)
-                if r >= reps // 3:
-                    ms.append(ex.last_kernel_ms())
-            kms = float(np.median(ms))
+            # as the headline: untimed launches first — at least 60 ms of them, so a
+            # compute-bound kernel (DOPRI5) is timed at the clock it sustains (C2: 0.57 ms per
+            # launch over the first 10 back-to-back launches, 0.49 over 50) — then K
+            # back-to-back launches without event markers, timed by two events on the stream
+            K = 20 if not n_stiff else 3
+            tw = time.perf_counter()
+            while True:
+                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True, timing=False)
+                if time.perf_counter() - tw > 0.06:
+                    break
+            sx = torch.cuda.current_stream(dev)
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(sx)
+            for _ in range(K):
+                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False)
+            ev[1].record(sx)
+            torch.cuda.synchronize(dev)
+            kms = ev[0].elapsed_time(ev[1]) / K
             byt = W * (T - 1) * 8 * Sx
             extra[name] = {"workload": f"{model} {method}, {W} walkers, trajectory mode"
                            + (f", {n_stiff} stiff walkers (tau=1e5)" if n_stiff else ""), "kernel_ms": kms,
+                           "timing": f"{K} back-to-back launches, events around them",
                            "walker_timesteps_per_s": W * (T - 1) / (kms / 1e3),
                            "hbm_frac": byt / (kms / 1e3) / 1e9 / HBM_PEAK_GBS}
             if n_stiff:

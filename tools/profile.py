@@ -100,7 +100,8 @@ def main():
     bl = summary["bench_line_under_profiler"]
     trace_csv = find(os.path.join(d, "**", "*kernel_trace.csv"))
     if bl and trace_csv:
-        hot = [r for r in read_csv(trace_csv) if "k_integrate<oe::TwoI, 0, true, true>" in r["Kernel_Name"]]
+        meth = {"rk4": 0, "dopri5": 1}[bl["config"]["method"]]
+        hot = [r for r in read_csv(trace_csv) if f"k_integrate<oe::TwoI, {meth}, true, true>" in r["Kernel_Name"]]
         hot.sort(key=lambda r: int(r["Start_Timestamp"]))
         w, k = bl["warmup"], bl["steps"]
         timed = hot[w:w + k]
