@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cached-stores", action="store_true", help="plain (cached) trajectory stores")
     ap.add_argument("--kernel", default="direct", choices=["direct", "pipe2", "pipe4", "pipe8"],
                     help="RK4 trajectory kernel (A/B of the opt-in producer/consumer variants)")
+    ap.add_argument("--xcd", default="runs", choices=["runs", "ranges", "off"],
+                    help="walker blocks per XCD: runs of 512 walkers (default), one range, blockIdx order")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mcmc-iters", type=int, default=21, help="MCMC leg iterations (0 = skip)")
@@ -86,6 +88,7 @@ def pmc_traffic(args):
 
 
 PIPE_ARG = {"direct": False, "pipe2": 2, "pipe4": 4, "pipe8": 8}
+XCD_ARG = {"runs": True, "ranges": "ranges", "off": False}
 
 
 def build_problem(model: str, method: str, T: int):
@@ -244,7 +247,8 @@ def main():
         # no timing-event markers between the timed launches (measured: markers between
         # back-to-back launches cost ~4 % of the C1 wall time, tools/launch_gaps.py)
         return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores,
-                             sync=False, timing=timing, pipelined=PIPE_ARG[args.kernel])
+                             sync=False, timing=timing, pipelined=PIPE_ARG[args.kernel],
+                             xcd_remap=XCD_ARG[args.xcd])
 
     for _ in range(args.warmup):
         step()
@@ -373,14 +377,16 @@ def main():
             K = 20 if not n_stiff else 3
             tw = time.perf_counter()
             while True:
-                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True, timing=False)
+                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True, timing=False,
+                                    xcd_remap=XCD_ARG[args.xcd])
                 if time.perf_counter() - tw > 0.06:
                     break
             sx = torch.cuda.current_stream(dev)
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(sx)
             for _ in range(K):
-                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False)
+                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False,
+                                    xcd_remap=XCD_ARG[args.xcd])
             ev[1].record(sx)
             torch.cuda.synchronize(dev)
             kms = ev[0].elapsed_time(ev[1]) / K
@@ -407,7 +413,7 @@ def main():
             "config": {"workload": f"{args.model} {args.method} trajectory-mode integrate + fused chi",
                        "walkers_per_gpu": Wl, "walkers_total": Wl * n_gpus, "states": S, "times": T,
                        "method": args.method, "stores": "cached" if args.cached_stores else "nontemporal",
-                       "kernel": args.kernel, "parallelism": f"walker-shard x{n_gpus}"},
+                       "kernel": args.kernel, "xcd": args.xcd, "parallelism": f"walker-shard x{n_gpus}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_s * 1e3, "kernel_ms_note": "timed-region event span / steps",

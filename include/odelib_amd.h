@@ -93,13 +93,16 @@ enum {
                          automatically for trajectories with S >= 5 at <= 1 wave per SIMD. */
   /* 32u: reserved (was an experimental split-wave layout, measured slower and removed) */
   OE_NO_XCD_REMAP = 64u, /* oe_integrate: keep blockIdx-order walker blocks.  By default the
-                           blocks an XCD receives (round-robin dispatch) take one contiguous
-                           range of walkers (same results, faster trajectory stores) */
+                           blocks the XCDs receive (round-robin dispatch) take runs of 512
+                           consecutive walkers in turn, so each XCD writes 4 KiB runs of every
+                           trajectory row (same results, faster trajectory stores) */
   OE_NO_TIMING = 128u,  /* oe_integrate: record no timing events around the launch (back-to-back
                            launches without event markers between them); oe_last_kernel_ms
                            then reports OE_ERR_STATE until a timed call */
   OE_PIPE_4 = 512u,     /* as OE_PIPE with 4 / 8 store waves per 4 compute waves (opt-in) */
-  OE_PIPE_8 = 1024u
+  OE_PIPE_8 = 1024u,
+  OE_XCD_RANGES = 2048u /* oe_integrate: one contiguous walker range per XCD instead (the r01
+                           mapping; same results) */
 };
 
 /* RNG modes for oe_mh_run */

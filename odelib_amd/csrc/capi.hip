@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <cmath>
 #include <cstdio>
@@ -481,7 +482,6 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   else if (flags & OE_PIPE) pipe_v = 0;
   const bool piped = pipe_v >= 0 && !e->rtc && c->method == OE_METHOD_RK4 && ia.traj && (W % 2 == 0) &&
                      e->rk4_piped[pipe_v][nt ? 1 : 0];
-  ia.xcd_remap = (flags & OE_NO_XCD_REMAP) ? 0 : 1;
   const bool timing = !(flags & OE_NO_TIMING);
   if (timing) OE_HIP(c, hipEventRecord(c->ev0, c->stream));
   if (piped) {
@@ -498,6 +498,16 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     ia.half = (rk4 && ((flags & OE_HALF_WAVES) || auto_half)) ? 1 : 0;
     const int64_t per_block = ia.half ? kBlock / 2 : kBlock;
     const dim3 grid((unsigned)((W + per_block - 1) / per_block)), block(kBlock);
+    // XCD runs of 512 walkers (4 KiB of each state row; OE_XCD_RUN_WALKERS overrides, for
+    // measurements), or one contiguous range per XCD
+    static const int64_t run_walkers = [] {
+      const char* v = getenv("OE_XCD_RUN_WALKERS");
+      const long n = v ? strtol(v, nullptr, 10) : 0;
+      return n > 0 ? (int64_t)n : (int64_t)512;
+    }();
+    ia.xcd_remap = (flags & OE_NO_XCD_REMAP) ? 0
+                   : (flags & OE_XCD_RANGES) ? (int32_t)std::max<int64_t>(1, (int64_t)grid.x / 8)
+                                             : (int32_t)std::max<int64_t>(1, run_walkers / per_block);
     OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));
   }
   OE_HIP(c, hipGetLastError());

@@ -731,17 +731,24 @@ struct IntegrateArgs {
   double* ssres;        // [W] or null
   int32_t* status;      // [W] or null
   int32_t half;         // 1: 32 walkers per wavefront (lanes 32-63 idle), 0: 64
-  int32_t xcd_remap;    // 1: the blocks dispatched to XCD x (blockIdx % 8, round-robin) take the
-                        //    x-th contiguous range of walker blocks (xcd_block)
+  int32_t xcd_remap;    // 0: walker blocks in blockIdx order; c > 0: the blocks dispatched to
+                        //    the 8 XCDs (blockIdx % 8, round-robin) take runs of c consecutive
+                        //    walker blocks in turn (xcd_block)
 };
 
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2).  Map
-// them so XCD x owns one contiguous range of walker blocks: each XCD's trajectory stores
-// then form long runs within every row instead of 2 KB pieces interleaved with the other
-// seven XCDs (measured 3-10 % faster).  A bijection on [0, G) for any G.
-__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t G) {
-  const int64_t q = G >> 3, r = G & 7, x = b & 7, j = b >> 3;
-  return x * q + (x < r ? x : r) + j;
+// them so the XCDs take runs of c consecutive walker blocks in turn: XCD x's j-th block
+// is block (j mod c) of run (j / c) * 8 + x.  With c blocks = 512 walkers every XCD writes
+// 4 KiB runs of each state row (pure [T][S][W] row stores, 65 536 walkers: 5.7-5.9 TB/s,
+// against 5.4-5.5 for one contiguous walker range per XCD and 4.7-4.9 for blockIdx order,
+// the 2 KiB pieces of a 256-walker block interleaved over the XCDs; tools/fill_bench.hip,
+// DESIGN.md §6).  Blocks past the last whole round of 8c keep their index: a bijection on
+// [0, G) for any G.  c = G/8 (G a multiple of 8) is one contiguous range per XCD.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t G, int32_t c) {
+  const int64_t full = G / (8 * c) * (8 * c);
+  if (b >= full) return b;
+  const int64_t x = b & 7, j = b >> 3;
+  return ((j / c) * 8 + x) * c + j % c;
 }
 
 // parameter registers: the model's own P plus up to 4 '<state>0' initial-condition
@@ -753,7 +760,7 @@ template <class M, int METHOD, bool TRAJ, bool NT>
 __global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const IntegrateArgs ia) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
-  const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x, ia.xcd_remap) : (int64_t)blockIdx.x;
   int64_t gw = blk * blockDim.x + threadIdx.x;
   bool idle = false;
   if (ia.half) {  // walker = (wave, lane < 32); the upper half-wave idles (DOPRI5: dead lanes)

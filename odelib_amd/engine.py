@@ -229,14 +229,15 @@ class Engine:
     # -- batched integrate -------------------------------------------------------------------
     def integrate(self, y0, theta, trajectory: bool = True, traj_out=None, nt_stores: bool = True,
                   sync: bool = True, pipelined=None, half_waves: bool = False,
-                  xcd_remap: bool = True, timing: bool = True):
+                  xcd_remap=True, timing: bool = True):
         """y0 [S][W], theta [P][W] → dict(traj [T][S][W] | None, chi [W], ssres [W], status [W]).
 
         ``pipelined=True`` (or 2, 4, 8: store waves per 4 compute waves) selects the
         opt-in producer/consumer RK4 trajectory kernel (same results).  ``half_waves=True`` runs
         32 walkers per wavefront (twice the waves; same results).
-        ``xcd_remap=False`` keeps blockIdx-order walker blocks instead of one contiguous
-        walker range per XCD (same results).  ``timing=False`` records no library events
+        ``xcd_remap=False`` keeps blockIdx-order walker blocks instead of runs of 512
+        walkers dealt to the XCDs in turn; ``xcd_remap="ranges"`` gives each XCD one
+        contiguous walker range (same results either way).  ``timing=False`` records no library events
         around the launch (``last_kernel_ms`` is then unavailable for this call)."""
         torch = self.torch
         pb = self.problem
@@ -257,7 +258,8 @@ class Engine:
         pipe = {None: 0, False: 0, True: N.OE_PIPE, 2: N.OE_PIPE, 4: N.OE_PIPE_4, 8: N.OE_PIPE_8}[pipelined]
         flags = N.OE_ASYNC | (N.OE_NT_STORES if nt_stores else 0) | pipe \
             | (N.OE_HALF_WAVES if half_waves else 0) \
-            | (0 if xcd_remap else N.OE_NO_XCD_REMAP) | (0 if timing else N.OE_NO_TIMING)
+            | (N.OE_XCD_RANGES if xcd_remap == "ranges" else 0 if xcd_remap else N.OE_NO_XCD_REMAP) \
+            | (0 if timing else N.OE_NO_TIMING)
         self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)
         if sync:
             torch.cuda.synchronize(self.dev)

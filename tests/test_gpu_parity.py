@@ -100,18 +100,22 @@ def test_rk4_half_waves_match_full_waves(spec, W):
 
 @pytest.mark.parametrize("method", ["rk4", "dopri5"])
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain5", "chain20"])
-@pytest.mark.parametrize("W", [1, 100, 4099, 8192])
+@pytest.mark.parametrize("W", [1, 100, 4099, 5000, 8192])
 def test_xcd_block_order_matches_blockidx_order(method, spec, W):
-    """XCD-contiguous walker blocks (the default) give the bits of blockIdx-order blocks
-    (trajectory, chi, R² residual, status), incl. ragged tails and odd S."""
+    """XCD runs of 512 walkers (the default) and one walker range per XCD give the bits of
+    blockIdx-order blocks (trajectory, chi, R² residual, status), incl. ragged tails, grids
+    that are not whole rounds of runs, half waves (chain5 RK4) and odd S."""
     m = _model(spec, method)
     theta = _walkers(spec, W)
     y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
     eng = m.engine()
     a = eng.integrate(y0, theta)
+    b = eng.integrate(y0, theta, xcd_remap="ranges")
     c = eng.integrate(y0, theta, xcd_remap=False)
     for key in ("traj", "chi", "ssres", "status"):
-        assert np.array_equal(c[key].cpu().numpy(), a[key].cpu().numpy(), equal_nan=True), key
+        ref = c[key].cpu().numpy()
+        assert np.array_equal(ref, a[key].cpu().numpy(), equal_nan=True), key
+        assert np.array_equal(ref, b[key].cpu().numpy(), equal_nan=True), key
 
 
 @pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain8"])

@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--cases", nargs="+", default=["two_i:rk4:65536", "two_i:dopri5:65536"])
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--modes", nargs="+", default=["traj", "notraj", "traj_half", "traj_noxcd"],
-                    help="traj/notraj + optional _half, _noxcd, _pipe / _pipe4 / _pipe8 (producer/consumer store waves), _auto (library choice; default: direct kernel)")
+                    help="traj/notraj + optional _half, _noxcd, _xcdrange (one walker range per XCD), _pipe / _pipe4 / _pipe8 (producer/consumer store waves), _auto (library choice; default: direct kernel)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -40,7 +40,8 @@ def main():
             for mode in modes:
                 eng.integrate(y0, theta, trajectory=mode.startswith("traj"),
                               traj_out=traj if mode.startswith("traj") else None, sync=True,
-                              half_waves="half" in mode, xcd_remap="noxcd" not in mode,
+                              half_waves="half" in mode,
+                              xcd_remap=False if "noxcd" in mode else "ranges" if "xcdrange" in mode else True,
                               pipelined=(8 if "pipe8" in mode else 4 if "pipe4" in mode else 2 if "pipe" in mode
                                          else None if "auto" in mode else False))
                 if r >= 3:
