@@ -103,7 +103,7 @@ def main():
         meth = {"rk4": 0, "dopri5": 1}[bl["config"]["method"]]
         hot = [r for r in read_csv(trace_csv) if f"k_integrate<oe::TwoI, {meth}, true, true>" in r["Kernel_Name"]]
         hot.sort(key=lambda r: int(r["Start_Timestamp"]))
-        w, k = bl["warmup"], bl["steps"]
+        w, k = bl.get("warmup_launches", bl["warmup"]), bl["steps"]
         timed = hot[w:w + k]
         if len(timed) == k:
             durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
