@@ -62,8 +62,9 @@ enum {
   OE_METHOD_AUTO = 2,   /* odeint's LSODA behaviour (Framework.py:656): DOPRI5 with a per-walker
                            stiffness test; stiff or over-budget walkers are integrated again by
                            the Rosenbrock method (status bit OE_STATUS_STIFF).  n_states <= 8 */
-  OE_METHOD_ROSENBROCK = 3 /* L-stable Rosenbrock 4(3) (ROS4) for every walker, exact Jacobian by
-                              dual numbers, steps ending on every output time.  n_states <= 8 */
+  OE_METHOD_ROSENBROCK = 3 /* stiffly accurate Rosenbrock 4(3) (RODAS) for every walker, exact
+                              Jacobian by dual numbers, continuous extension onto the output
+                              times.  n_states <= 8 */
 };
 
 /* built-in right-hand sides (demo notebook models + synthetic chain) */

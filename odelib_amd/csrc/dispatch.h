@@ -16,7 +16,7 @@ struct Entry {
   int32_t model_id;
   int32_t S;
   int32_t P;  // the model's own parameter count
-  // [method][traj][nt]; methods kAuto / kRos4 are null when S > kStiffMaxS
+  // [method][traj][nt]; methods kAuto / kRosenbrock are null when S > kStiffMaxS
   IntegrateLaunch integrate[4][2][2];
   IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > 8
   MHLaunch mh[4];
@@ -79,7 +79,7 @@ Entry make_entry(int32_t model_id) {
   fill_method<M, kDOPRI5>(e);
   if constexpr (M::S <= kStiffMaxS) {
     fill_method<M, kAuto>(e);
-    fill_method<M, kRos4>(e);
+    fill_method<M, kRosenbrock>(e);
   }
   if constexpr (M::S <= 8) {
     e.rk4_piped[0][0] = launch_rk4_piped<M, false, 2>;

@@ -59,7 +59,7 @@ enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8
 
 // integrators (OE_METHOD_*): fixed-step RK4, DOPRI5, DOPRI5 with stiffness detection and
 // the Rosenbrock fallback for stiff / over-budget walkers (LSODA-like), Rosenbrock only
-enum : int { kRK4 = 0, kDOPRI5 = 1, kAuto = 2, kRos4 = 3 };
+enum : int { kRK4 = 0, kDOPRI5 = 1, kAuto = 2, kRosenbrock = 3 };
 constexpr int kStiffMaxS = 8;  // the stiff methods factor an S x S matrix per lane in registers
 constexpr int kStiffTestSteps = 3;  // auto: stiffness test from the 3rd step within one output interval
 
@@ -712,10 +712,10 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
         a = acc_init();
         a.status = ST_STIFF;
       }
-      integrate_ros4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, redo, a);
+      integrate_rosenbrock<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, redo, a);
     }
-  } else {  // kRos4: the Rosenbrock method for every walker
-    integrate_ros4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, active, a);
+  } else {  // kRosenbrock: the Rosenbrock method for every walker
+    integrate_rosenbrock<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, active, a);
   }
 }
 

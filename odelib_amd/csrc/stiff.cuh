@@ -2,9 +2,9 @@
 //
 // LSODA integrates with Adams methods and switches to BDF when it detects stiffness.
 // Here the non-stiff integrator is the wave-lockstep DOPRI5 (ode_kernels.cuh); the
-// stiff integrator is an L-stable Rosenbrock method of order 4 with an embedded order-3
-// error estimate (Hairer & Wanner, Solving ODEs II, §IV.7, the 4-stage ROS4 family in the
-// Kaps–Rentrop form with γ = 0.57282, three RHS evaluations per step).  The method
+// stiff integrator is the stiffly accurate Rosenbrock method RODAS of order 4 with an
+// L-stable embedded order-3 error estimate and an order-3 continuous extension (Hairer &
+// Wanner, Solving ODEs II, §VI.4; γ = 0.25, 6 stages, 5 RHS evaluations per step).  The method
 // 'auto' (OE_METHOD_AUTO) runs DOPRI5 with Hairer's per-lane stiffness test
 // (h·|λ| ≥ 3.25 on 15 accepted steps in a row) and evicts stiff lanes — and lanes over
 // the step budget — from the wave; those walkers are then integrated again from t0 by
@@ -16,12 +16,12 @@
 //   * Linear algebra: (1/(γh) I − J) is factored per lane in registers (LU with threshold
 //     partial pivoting; row swaps by selects, so nothing is indexed by a per-lane value,
 //     skipped by a wave none of whose lanes needs them).
-//   * Output: steps end on every grid time (no interpolation; stiff components make
-//     Hermite interpolation from f useless), so each row is a step endpoint.
+//   * Output: the method's own continuous extension (from the stage increments, valid on
+//     stiff components, unlike Hermite interpolation from f) for grid times inside a
+//     step; a grid time on a step's end takes the new state.
 //   * Step control: max-norm error as DOPRI5, fac = 0.9·err^(−1/4) in [0.2, 6], wave
 //     maximum over the participating lanes; eviction as DOPRI5, with a step budget of
-//     kRosBudget × max_steps per output interval (an order-4 method takes several times
-//     LSODA's BDF steps through a stiff transient at odeint's tolerances).
+//     kRosBudget × max_steps per output interval.
 // Everything is IEEE add/mul/fma/div plus frexp/ldexp, restated operation for operation
 // in oracle/rk_ref.c, so the kernel is bitwise testable.
 #pragma once
@@ -178,18 +178,31 @@ __device__ __forceinline__ void jac_eval(const double (&y)[M::S], double t, cons
   }
 }
 
-// ---- ROS4, L-stable parameter set (Hairer & Wanner II, §IV.7), Kaps–Rentrop form ----
+// ---- RODAS (Hairer & Wanner II, §VI.4): Rosenbrock 4(3), 6 stages, stiffly accurate ----
+// Both the solution and the embedded order-3 solution are L-stable, so the error
+// estimate (the last stage increment k6) stays small on stiff components that sit on
+// their slow manifold.  An order-4 method whose embedded estimate is not L-stable (the
+// 4-stage ROS4 family used before) reads the O(ε) manifold offset of a fast component as
+// error and takes ~8x the steps at odeint's tolerances (two_i with τ = 1e5: 14 200 steps
+// vs 1 640).  Stages 5 and 6 are evaluated at t + h; the continuous
+// extension (order 3) gives the grid points inside a step, so steps need not end on them.
 namespace ros {
-constexpr double gam = 0.57282;
-constexpr double a21 = 2.0, a31 = 1.867943637803922, a32 = 0.2344449711399156;
-constexpr double c21 = -7.137615036412310, c31 = 2.580708087951457, c32 = 0.6515950076447975,
-                 c41 = -2.137148994382534, c42 = -0.3214669691237626, c43 = -0.6949742501781779;
-constexpr double m1 = 2.255570073418735, m2 = 0.2870493262186792, m3 = 0.435317943184018, m4 = 1.093502252409163;
-constexpr double e1 = -0.2815431932141155, e2 = -0.0727619912493892, e3 = -0.1082196201495311,
-                 e4 = -1.093502252409163;
-constexpr double a2x = 1.14564, a3x = 0.65521686381559;
-constexpr double g1x = 0.57282, g2x = -1.769193891319233, g3x = 0.7592633437920482, g4x = -0.104902108710045;
-constexpr double inv_gam = 1.0 / gam;
+constexpr double gam = 0.25;
+constexpr double inv_gam = 4.0;
+constexpr double a21 = 1.544, a31 = 0.9466785280815826, a32 = 0.2557011698983284, a41 = 3.314825187068521,
+                 a42 = 2.896124015972201, a43 = 0.9986419139977817, a51 = 1.221224509226641,
+                 a52 = 6.019134481288629, a53 = 12.53708332932087, a54 = -0.687886036105895;
+constexpr double c21 = -5.6688, c31 = -2.430093356833875, c32 = -0.2063599157091915, c41 = -0.1073529058151375,
+                 c42 = -9.594562251023355, c43 = -20.47028614809616, c51 = 7.496443313967647,
+                 c52 = -10.24680431464352, c53 = -33.99990352819905, c54 = 11.7089089320616,
+                 c61 = 8.083246795921522, c62 = -7.981132988064893, c63 = -31.52159432874371,
+                 c64 = 16.31930543123136, c65 = -6.058818238834054;
+constexpr double c2x = 0.386, c3x = 0.21, c4x = 0.63;                      // stage times (α_i)
+constexpr double d1 = 0.25, d2 = -0.1043, d3 = 0.1035, d4 = -0.03620000000000023;  // ∂f/∂t weights (γ_i)
+constexpr double h21 = 10.12623508344586, h22 = -7.487995877610167, h23 = -34.80091861555747,
+                 h24 = -7.992771707568823, h25 = 1.025137723295662;         // dense output
+constexpr double h31 = -0.6762803392801253, h32 = 6.087714651680015, h33 = 16.43084320892478,
+                 h34 = 24.76722511418386, h35 = -6.594389125716872;
 constexpr double safe = 0.9, facmin = 0.2, facmax = 6.0;
 constexpr int kRosBudget = 8;  // step budget per output interval, in units of max_steps
 
@@ -296,13 +309,14 @@ __device__ __forceinline__ void lu_solve(const double (&a)[S][S], const int (&pi
 }
 }  // namespace ros
 
-// Rosenbrock integration of the lanes with `part` set (the others sit out: they neither
-// steer the step size nor emit).  Wave-lockstep: one step size per wave, steps end on
-// every grid time.  y is the initial state on entry and the final state on return.
+// Rosenbrock (RODAS) integration of the lanes with `part` set (the others sit out: they
+// neither steer the step size nor emit).  Wave-lockstep: one step size per wave; grid
+// points inside a step come from the continuous extension, a grid point on the step's
+// end is the new state itself.  y is the initial state on entry, the final on return.
 template <class M, int PMAX, bool TRAJ, bool NT>
-__device__ __forceinline__ void integrate_ros4(const DevProblem& pb, double (&y)[M::S], const double (&p)[PMAX],
-                                               double* traj, int64_t W, uint32_t off, bool active, bool part,
-                                               Acc& a) {
+__device__ __forceinline__ void integrate_rosenbrock(const DevProblem& pb, double (&y)[M::S],
+                                                     const double (&p)[PMAX], double* traj, int64_t W,
+                                                     uint32_t off, bool active, bool part, Acc& a) {
   using namespace ros;
   constexpr int S = M::S;
   const cptr<double> times = kconst(pb.times);
@@ -352,15 +366,14 @@ __device__ __forceinline__ void integrate_ros4(const DevProblem& pb, double (&y)
   int i = 1, nst = 0;
   bool last_rej = false;
   while (i < pb.T) {
-    const double ti = times[i];
-    const double hp = h;
-    bool clip = false;
-    if (t + h >= ti) { h = ti - t; clip = true; }
+    bool last = false;
+    if (t + h >= tend) { h = tend - t; last = true; }
     const double rh = 1.0 / h;
     const double gh = rh * inv_gam;
     const double c21h = c21 * rh, c31h = c31 * rh, c32h = c32 * rh, c41h = c41 * rh, c42h = c42 * rh,
-                 c43h = c43 * rh;
-    const double hg1 = h * g1x, hg2 = h * g2x, hg3 = h * g3x, hg4 = h * g4x;
+                 c43h = c43 * rh, c51h = c51 * rh, c52h = c52 * rh, c53h = c53 * rh, c54h = c54 * rh,
+                 c61h = c61 * rh, c62h = c62 * rh, c63h = c63 * rh, c64h = c64 * rh, c65h = c65 * rh;
+    const double hd1 = h * d1, hd2 = h * d2, hd3 = h * d3, hd4 = h * d4;
     double lu[S][S], dinv[S];
     int piv[S];
 #pragma unroll
@@ -368,32 +381,47 @@ __device__ __forceinline__ void integrate_ros4(const DevProblem& pb, double (&y)
 #pragma unroll
       for (int c = 0; c < S; ++c) lu[r][c] = (r == c) ? gh - J[r][c] : -J[r][c];
     const bool any_swap = lu_factor<S>(lu, piv, dinv);
-    double g1[S], g2[S], g3[S], g4[S], yt[S], fv[S];
+    double k1[S], k2[S], k3[S], k4[S], k5[S], k6[S], yt[S], fv[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) g1[s] = fma(hg1, ft[s], f0[s]);
-    lu_solve<S>(lu, piv, dinv, any_swap, g1);
+    for (int s = 0; s < S; ++s) k1[s] = fma(hd1, ft[s], f0[s]);
+    lu_solve<S>(lu, piv, dinv, any_swap, k1);
 #pragma unroll
-    for (int s = 0; s < S; ++s) yt[s] = fma(a21, g1[s], y[s]);
-    M::rhs(yt, t + a2x * h, p, fv);
+    for (int s = 0; s < S; ++s) yt[s] = fma(a21, k1[s], y[s]);
+    M::rhs(yt, t + c2x * h, p, fv);
 #pragma unroll
-    for (int s = 0; s < S; ++s) g2[s] = fma(hg2, ft[s], fma(c21h, g1[s], fv[s]));
-    lu_solve<S>(lu, piv, dinv, any_swap, g2);
+    for (int s = 0; s < S; ++s) k2[s] = fma(hd2, ft[s], fma(c21h, k1[s], fv[s]));
+    lu_solve<S>(lu, piv, dinv, any_swap, k2);
 #pragma unroll
-    for (int s = 0; s < S; ++s) yt[s] = fma(a32, g2[s], fma(a31, g1[s], y[s]));
-    M::rhs(yt, t + a3x * h, p, fv);
+    for (int s = 0; s < S; ++s) yt[s] = fma(a32, k2[s], fma(a31, k1[s], y[s]));
+    M::rhs(yt, t + c3x * h, p, fv);
 #pragma unroll
-    for (int s = 0; s < S; ++s) g3[s] = fma(hg3, ft[s], fma(c32h, g2[s], fma(c31h, g1[s], fv[s])));
-    lu_solve<S>(lu, piv, dinv, any_swap, g3);
+    for (int s = 0; s < S; ++s) k3[s] = fma(hd3, ft[s], fma(c32h, k2[s], fma(c31h, k1[s], fv[s])));
+    lu_solve<S>(lu, piv, dinv, any_swap, k3);
 #pragma unroll
-    for (int s = 0; s < S; ++s) g4[s] = fma(hg4, ft[s], fma(c43h, g3[s], fma(c42h, g2[s], fma(c41h, g1[s], fv[s]))));
-    lu_solve<S>(lu, piv, dinv, any_swap, g4);
+    for (int s = 0; s < S; ++s) yt[s] = fma(a43, k3[s], fma(a42, k2[s], fma(a41, k1[s], y[s])));
+    M::rhs(yt, t + c4x * h, p, fv);
+#pragma unroll
+    for (int s = 0; s < S; ++s) k4[s] = fma(hd4, ft[s], fma(c43h, k3[s], fma(c42h, k2[s], fma(c41h, k1[s], fv[s]))));
+    lu_solve<S>(lu, piv, dinv, any_swap, k4);
+#pragma unroll
+    for (int s = 0; s < S; ++s) yt[s] = fma(a54, k4[s], fma(a53, k3[s], fma(a52, k2[s], fma(a51, k1[s], y[s]))));
+    M::rhs(yt, t + h, p, fv);
+#pragma unroll
+    for (int s = 0; s < S; ++s) k5[s] = fma(c54h, k4[s], fma(c53h, k3[s], fma(c52h, k2[s], fma(c51h, k1[s], fv[s]))));
+    lu_solve<S>(lu, piv, dinv, any_swap, k5);
+#pragma unroll
+    for (int s = 0; s < S; ++s) yt[s] = yt[s] + k5[s];  // the embedded solution
+    M::rhs(yt, t + h, p, fv);
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      k6[s] = fma(c65h, k5[s], fma(c64h, k4[s], fma(c63h, k3[s], fma(c62h, k2[s], fma(c61h, k1[s], fv[s])))));
+    lu_solve<S>(lu, piv, dinv, any_swap, k6);
     double y1[S];
     double num = 0.0, den = 1.0, nfe = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      y1[s] = fma(m4, g4[s], fma(m3, g3[s], fma(m2, g2[s], fma(m1, g1[s], y[s]))));
-      const double e = fma(e4, g4[s], fma(e3, g3[s], fma(e2, g2[s], e1 * g1[s])));
-      const double ae = fabs(e);
+      y1[s] = yt[s] + k6[s];
+      const double ae = fabs(k6[s]);  // solution minus embedded solution
       const double sk = fma(rtol, max_abs_raw(y[s], y1[s]), atol);
       nfe = fma(ae, 0.0, nfe);
       nfe = fma(y1[s], 0.0, nfe);
@@ -405,12 +433,32 @@ __device__ __forceinline__ void integrate_ros4(const DevProblem& pb, double (&y)
     const double err = wave_max(el);
     ++nst;
     if (err <= 1.0) {
-      const double tn = clip ? ti : t + h;
+      const double tn = last ? tend : t + h;
+      if (i < pb.T && times[i] < tn) {  // wave-uniform: a grid point inside the step
+        double q3[S], q4[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          q3[s] = fma(h25, k5[s], fma(h24, k4[s], fma(h23, k3[s], fma(h22, k2[s], h21 * k1[s]))));
+          q4[s] = fma(h35, k5[s], fma(h34, k4[s], fma(h33, k3[s], fma(h32, k2[s], h31 * k1[s]))));
+        }
+        while (i < pb.T && times[i] < tn) {
+          if (part && grid_needs_emit<S, TRAJ>(pb, i, k)) {
+            const double th = (times[i] - t) * rh;
+            const double th1 = 1.0 - th;
+            double yo[S];
+#pragma unroll
+            for (int s = 0; s < S; ++s) yo[s] = fma(th, fma(th1, fma(th, q4[s], q3[s]), y1[s]), th1 * y[s]);
+            emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, emit_ok, k, a);
+          }
+          ++i;
+          nst = 0;
+        }
+      }
 #pragma unroll
       for (int s = 0; s < S; ++s) y[s] = part ? y1[s] : y[s];  // bystanders keep their state
       t = tn;
-      if (clip) {
-        if (part) emit<S, TRAJ, NT>(pb, i, y, traj, W, off, emit_ok, k, a);
+      if (i < pb.T && times[i] == tn) {  // a grid point on the step's end
+        if (part && grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, y, traj, W, off, emit_ok, k, a);
         ++i;
         nst = 0;
       }
@@ -418,9 +466,7 @@ __device__ __forceinline__ void integrate_ros4(const DevProblem& pb, double (&y)
       double fac = (err > 0.0) ? safe * inv_fourth_root(err) : facmax;
       fac = fmin(facmax, fmax(facmin, fac));
       if (last_rej) fac = fmin(fac, 1.0);
-      const double hn = h * fac;
-      // a step cut short by the grid does not shrink the planned step
-      h = clip ? fmax(hn, hp) : hn;
+      h = h * fac;
       last_rej = false;
     } else {
       h = h * fmax(facmin, safe * inv_fourth_root(err));
@@ -440,7 +486,7 @@ __device__ __forceinline__ void integrate_ros4(const DevProblem& pb, double (&y)
 #pragma unroll
         for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
         for (; i < pb.T; ++i)
-          if (part) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, emit_ok, k, a);
+          if (part && grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, emit_ok, k, a);
         break;
       }
       if (h < hmin) h = fmin(1e-3 * span, tend - t);

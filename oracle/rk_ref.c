@@ -17,10 +17,10 @@
  *   - the batched Metropolis–Hastings step (Samplers.py:104-153) with replay or
  *     Philox4x32-10 draws;
  *   - the stiff methods: DOPRI5 with Hairer's stiffness test and
- *     eviction ('auto'), and the L-stable ROS4 Rosenbrock method (Hairer & Wanner II
- *     §IV.7) with the Jacobian from forward-mode dual numbers through the model RHS,
- *     LU with partial pivoting, steps ending on every grid time, for 64-lane groups
- *     sharing one step size.
+ *     eviction ('auto'), and the stiffly accurate Rosenbrock method RODAS (Hairer &
+ *     Wanner II §VI.4) with the Jacobian from forward-mode dual numbers through the model
+ *     RHS, LU with threshold partial pivoting and the method's continuous extension onto
+ *     the grid, for 64-lane groups sharing one step size.
  */
 #include <math.h>
 #include <stdint.h>
@@ -33,7 +33,7 @@
 
 enum { M_ZERO_I = 0, M_ONE_I = 1, M_TWO_I = 2, M_CHAIN = 3 };
 enum { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8 };
-enum { METHOD_RK4 = 0, METHOD_DOPRI5 = 1, METHOD_AUTO = 2, METHOD_ROS4 = 3 };
+enum { METHOD_RK4 = 0, METHOD_DOPRI5 = 1, METHOD_AUTO = 2, METHOD_ROSENBROCK = 3 };
 
 typedef struct {
   int model, S, P, T;
@@ -186,7 +186,7 @@ typedef struct {
   Acc a;
   int kobs;
   int n_stiff, n_nonstiff; /* auto: consecutive stiff / non-stiff accepted steps */
-  int part;                /* ros4: lane takes part in the stiff integration */
+  int part;                /* rosenbrock: lane takes part in the stiff integration */
   double y0c[MAXS];        /* auto: initial state, for the restart */
 } Lane;
 
@@ -492,15 +492,23 @@ static void jac_eval(const Prob* pb, const double* y, double t, const double* p,
   }
 }
 
-/* ROS4, L-stable set (Hairer & Wanner II §IV.7), Kaps-Rentrop form */
-static const double r_gam = 0.57282, r_a21 = 2.0, r_a31 = 1.867943637803922, r_a32 = 0.2344449711399156,
-                    r_c21 = -7.137615036412310, r_c31 = 2.580708087951457, r_c32 = 0.6515950076447975,
-                    r_c41 = -2.137148994382534, r_c42 = -0.3214669691237626, r_c43 = -0.6949742501781779,
-                    r_m1 = 2.255570073418735, r_m2 = 0.2870493262186792, r_m3 = 0.435317943184018,
-                    r_m4 = 1.093502252409163, r_e1 = -0.2815431932141155, r_e2 = -0.0727619912493892,
-                    r_e3 = -0.1082196201495311, r_e4 = -1.093502252409163, r_a2x = 1.14564,
-                    r_a3x = 0.65521686381559, r_g1x = 0.57282, r_g2x = -1.769193891319233,
-                    r_g3x = 0.7592633437920482, r_g4x = -0.104902108710045;
+/* RODAS (Hairer & Wanner II §VI.4): stiffly accurate Rosenbrock 4(3), 6 stages, L-stable
+   embedded estimate, order-3 continuous extension (stiff.cuh namespace ros) */
+static const double r_inv_gam = 4.0, r_a21 = 1.544, r_a31 = 0.9466785280815826, r_a32 = 0.2557011698983284,
+                    r_a41 = 3.314825187068521, r_a42 = 2.896124015972201, r_a43 = 0.9986419139977817,
+                    r_a51 = 1.221224509226641, r_a52 = 6.019134481288629, r_a53 = 12.53708332932087,
+                    r_a54 = -0.687886036105895;
+static const double r_c21 = -5.6688, r_c31 = -2.430093356833875, r_c32 = -0.2063599157091915,
+                    r_c41 = -0.1073529058151375, r_c42 = -9.594562251023355, r_c43 = -20.47028614809616,
+                    r_c51 = 7.496443313967647, r_c52 = -10.24680431464352, r_c53 = -33.99990352819905,
+                    r_c54 = 11.7089089320616, r_c61 = 8.083246795921522, r_c62 = -7.981132988064893,
+                    r_c63 = -31.52159432874371, r_c64 = 16.31930543123136, r_c65 = -6.058818238834054;
+static const double r_c2x = 0.386, r_c3x = 0.21, r_c4x = 0.63;
+static const double r_d1 = 0.25, r_d2 = -0.1043, r_d3 = 0.1035, r_d4 = -0.03620000000000023;
+static const double r_h21 = 10.12623508344586, r_h22 = -7.487995877610167, r_h23 = -34.80091861555747,
+                    r_h24 = -7.992771707568823, r_h25 = 1.025137723295662, r_h31 = -0.6762803392801253,
+                    r_h32 = 6.087714651680015, r_h33 = 16.43084320892478, r_h34 = 24.76722511418386,
+                    r_h35 = -6.594389125716872;
 
 /* x^(-1/4), same operations as stiff.cuh inv_fourth_root (bit-identical) */
 static double inv_fourth_root(double x) {
@@ -561,16 +569,18 @@ static void lu_solve(int S, const double* a, const int* piv, const double* dinv,
 }
 
 typedef struct {
-  double f0[MAXS], J[MAXS * MAXS], ft[MAXS], y1[MAXS];
+  double f0[MAXS], J[MAXS * MAXS], ft[MAXS], y1[MAXS], q3[MAXS], q4[MAXS];
 } RosLane;
 
-/* Rosenbrock over a 64-lane group: lanes with part set integrate from their L[l].y,
-   the others sit out (no emit, no vote on the step size) */
-static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
+/* Rosenbrock (RODAS) over a 64-lane group: lanes with part set integrate from their
+   L[l].y, the others sit out (no emit, no vote on the step size).  Grid points inside a
+   step from the continuous extension, a grid point on the step's end = the new state. */
+static void rodas_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
   static __thread RosLane R[LANES];
   const int S = pb->S;
   const double t0 = pb->times[0], tend = pb->times[pb->T - 1];
   const double rtol = pb->rtol, atol = pb->atol;
+  const int tr = traj != NULL;
   double t = t0;
   for (int l = 0; l < nl; ++l) {
     Lane* q = &L[l];
@@ -609,18 +619,16 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
   h = fmin(h, tend - t0);
   const double span = tend - t0;
   const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
-  const double inv_gam = 1.0 / r_gam;
   const int budget = 8 * pb->max_steps; /* stiff.cuh kRosBudget */
   int i = 1, nst = 0, last_rej = 0;
   while (i < pb->T) {
-    const double ti = pb->times[i];
-    const double hp = h;
-    int clip = 0;
-    if (t + h >= ti) { h = ti - t; clip = 1; }
-    const double rh = 1.0 / h, gh = rh * inv_gam;
+    int last = 0;
+    if (t + h >= tend) { h = tend - t; last = 1; }
+    const double rh = 1.0 / h, gh = rh * r_inv_gam;
     const double c21h = r_c21 * rh, c31h = r_c31 * rh, c32h = r_c32 * rh, c41h = r_c41 * rh, c42h = r_c42 * rh,
-                 c43h = r_c43 * rh;
-    const double hg1 = h * r_g1x, hg2 = h * r_g2x, hg3 = h * r_g3x, hg4 = h * r_g4x;
+                 c43h = r_c43 * rh, c51h = r_c51 * rh, c52h = r_c52 * rh, c53h = r_c53 * rh, c54h = r_c54 * rh,
+                 c61h = r_c61 * rh, c62h = r_c62 * rh, c63h = r_c63 * rh, c64h = r_c64 * rh, c65h = r_c65 * rh;
+    const double hd1 = h * r_d1, hd2 = h * r_d2, hd3 = h * r_d3, hd4 = h * r_d4;
     for (int l = 0; l < nl; ++l) {
       Lane* q = &L[l];
       RosLane* rl = &R[l];
@@ -632,45 +640,72 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
       for (int r = 0; r < S; ++r)
         for (int c = 0; c < S; ++c) lu[r * S + c] = (r == c) ? gh - rl->J[r * S + c] : -rl->J[r * S + c];
       lu_factor(S, lu, piv, dinv);
-      double g1[MAXS], g2[MAXS], g3[MAXS], g4[MAXS], yt[MAXS], fv[MAXS];
-      for (int s = 0; s < S; ++s) g1[s] = fma(hg1, rl->ft[s], rl->f0[s]);
-      lu_solve(S, lu, piv, dinv, g1);
-      for (int s = 0; s < S; ++s) yt[s] = fma(r_a21, g1[s], q->y[s]);
-      rhs(pb, yt, t + r_a2x * h, pl, fv);
-      for (int s = 0; s < S; ++s) g2[s] = fma(hg2, rl->ft[s], fma(c21h, g1[s], fv[s]));
-      lu_solve(S, lu, piv, dinv, g2);
-      for (int s = 0; s < S; ++s) yt[s] = fma(r_a32, g2[s], fma(r_a31, g1[s], q->y[s]));
-      rhs(pb, yt, t + r_a3x * h, pl, fv);
-      for (int s = 0; s < S; ++s) g3[s] = fma(hg3, rl->ft[s], fma(c32h, g2[s], fma(c31h, g1[s], fv[s])));
-      lu_solve(S, lu, piv, dinv, g3);
+      double k1[MAXS], k2[MAXS], k3[MAXS], k4[MAXS], k5[MAXS], k6[MAXS], yt[MAXS], fv[MAXS];
+      const double* y = q->y;
+      for (int s = 0; s < S; ++s) k1[s] = fma(hd1, rl->ft[s], rl->f0[s]);
+      lu_solve(S, lu, piv, dinv, k1);
+      for (int s = 0; s < S; ++s) yt[s] = fma(r_a21, k1[s], y[s]);
+      rhs(pb, yt, t + r_c2x * h, pl, fv);
+      for (int s = 0; s < S; ++s) k2[s] = fma(hd2, rl->ft[s], fma(c21h, k1[s], fv[s]));
+      lu_solve(S, lu, piv, dinv, k2);
+      for (int s = 0; s < S; ++s) yt[s] = fma(r_a32, k2[s], fma(r_a31, k1[s], y[s]));
+      rhs(pb, yt, t + r_c3x * h, pl, fv);
+      for (int s = 0; s < S; ++s) k3[s] = fma(hd3, rl->ft[s], fma(c32h, k2[s], fma(c31h, k1[s], fv[s])));
+      lu_solve(S, lu, piv, dinv, k3);
+      for (int s = 0; s < S; ++s) yt[s] = fma(r_a43, k3[s], fma(r_a42, k2[s], fma(r_a41, k1[s], y[s])));
+      rhs(pb, yt, t + r_c4x * h, pl, fv);
       for (int s = 0; s < S; ++s)
-        g4[s] = fma(hg4, rl->ft[s], fma(c43h, g3[s], fma(c42h, g2[s], fma(c41h, g1[s], fv[s]))));
-      lu_solve(S, lu, piv, dinv, g4);
+        k4[s] = fma(hd4, rl->ft[s], fma(c43h, k3[s], fma(c42h, k2[s], fma(c41h, k1[s], fv[s]))));
+      lu_solve(S, lu, piv, dinv, k4);
+      for (int s = 0; s < S; ++s)
+        yt[s] = fma(r_a54, k4[s], fma(r_a53, k3[s], fma(r_a52, k2[s], fma(r_a51, k1[s], y[s]))));
+      rhs(pb, yt, t + h, pl, fv);
+      for (int s = 0; s < S; ++s)
+        k5[s] = fma(c54h, k4[s], fma(c53h, k3[s], fma(c52h, k2[s], fma(c51h, k1[s], fv[s]))));
+      lu_solve(S, lu, piv, dinv, k5);
+      for (int s = 0; s < S; ++s) yt[s] = yt[s] + k5[s];
+      rhs(pb, yt, t + h, pl, fv);
+      for (int s = 0; s < S; ++s)
+        k6[s] = fma(c65h, k5[s], fma(c64h, k4[s], fma(c63h, k3[s], fma(c62h, k2[s], fma(c61h, k1[s], fv[s])))));
+      lu_solve(S, lu, piv, dinv, k6);
       double num = 0.0, den = 1.0, nfe = 0.0;
       for (int s = 0; s < S; ++s) {
-        rl->y1[s] = fma(r_m4, g4[s], fma(r_m3, g3[s], fma(r_m2, g2[s], fma(r_m1, g1[s], q->y[s]))));
-        double e = fma(r_e4, g4[s], fma(r_e3, g3[s], fma(r_e2, g2[s], r_e1 * g1[s])));
-        double ae = fabs(e);
-        double sk = fma(rtol, fmax(fabs(q->y[s]), fabs(rl->y1[s])), atol);
+        rl->y1[s] = yt[s] + k6[s];
+        double ae = fabs(k6[s]);
+        double sk = fma(rtol, fmax(fabs(y[s]), fabs(rl->y1[s])), atol);
         nfe = fma(ae, 0.0, nfe);
         nfe = fma(rl->y1[s], 0.0, nfe);
         if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
+        rl->q3[s] = fma(r_h25, k5[s], fma(r_h24, k4[s], fma(r_h23, k3[s], fma(r_h22, k2[s], r_h21 * k1[s]))));
+        rl->q4[s] = fma(r_h35, k5[s], fma(r_h34, k4[s], fma(r_h33, k3[s], fma(r_h32, k2[s], r_h31 * k1[s]))));
       }
       double el = num / den;
       if (!isfinite(el) || isnan(nfe)) el = 1e30;
-      if (q->dead) el = 0.0;
       q->el = el;
     }
     double err = grp_max(L, nl, 1);
     ++nst;
     if (err <= 1.0) {
-      const double tn = clip ? ti : t + h;
+      const double tn = last ? tend : t + h;
+      while (i < pb->T && pb->times[i] < tn) {
+        const double th = (pb->times[i] - t) * rh, th1 = 1.0 - th;
+        for (int l = 0; l < nl; ++l) {
+          Lane* q = &L[l];
+          if (!q->part || !needs_emit(pb, tr, i, q->kobs)) continue;
+          double yo[MAXS];
+          for (int s = 0; s < S; ++s) yo[s] = fma(th, fma(th1, fma(th, R[l].q4[s], R[l].q3[s]), R[l].y1[s]), th1 * q->y[s]);
+          emit(pb, i, yo, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
+        }
+        ++i;
+        nst = 0;
+      }
       for (int l = 0; l < nl; ++l)
         if (L[l].part && !L[l].dead) memcpy(L[l].y, R[l].y1, sizeof(double) * S); /* evicted: stays NaN */
       t = tn;
-      if (clip) {
+      if (i < pb->T && pb->times[i] == tn) {
         for (int l = 0; l < nl; ++l)
-          if (L[l].part) emit(pb, i, L[l].y, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
+          if (L[l].part && needs_emit(pb, tr, i, L[l].kobs))
+            emit(pb, i, L[l].y, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
         ++i;
         nst = 0;
       }
@@ -680,8 +715,7 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
       double fac = (err > 0.0) ? 0.9 * inv_fourth_root(err) : 6.0;
       fac = fmin(6.0, fmax(0.2, fac));
       if (last_rej) fac = fmin(fac, 1.0);
-      const double hn = h * fac;
-      h = clip ? fmax(hn, hp) : hn;
+      h = h * fac;
       last_rej = 0;
     } else {
       h = h * fmax(0.2, 0.9 * inv_fourth_root(err));
@@ -702,7 +736,8 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
         for (int s = 0; s < S; ++s) yo[s] = NAN;
         for (; i < pb->T; ++i)
           for (int l = 0; l < nl; ++l)
-            if (L[l].part) emit(pb, i, yo, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
+            if (L[l].part && needs_emit(pb, tr, i, L[l].kobs))
+              emit(pb, i, yo, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
         break;
       }
       if (h < hmin) h = fmin(1e-3 * span, tend - t);
@@ -712,7 +747,7 @@ static void ros4_group(const Prob* pb, Lane* L, int nl, const double* p, double*
     if (L[l].part) check_finite(S, L[l].y, &L[l].a);
 }
 
-/* 'auto': DOPRI5 with the stiffness test, then the evicted walkers again from t0 by ROS4 */
+/* 'auto': DOPRI5 with the stiffness test, then the evicted walkers again from t0 by RODAS */
 static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
   const int S = pb->S;
   for (int l = 0; l < nl; ++l) memcpy(L[l].y0c, L[l].y, sizeof(double) * S);
@@ -729,7 +764,7 @@ static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double*
       acc_init(&L[l].a);
       L[l].a.status = ST_STIFF;
     }
-  ros4_group(pb, L, nl, p, traj, W);
+  rodas_group(pb, L, nl, p, traj, W);
 }
 
 static Prob make_prob(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
@@ -776,7 +811,7 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
     auto_group(pb, L, LANES, p, traj, W);
   } else {
     for (int l = 0; l < LANES; ++l) L[l].part = L[l].active;
-    ros4_group(pb, L, LANES, p, traj, W);
+    rodas_group(pb, L, LANES, p, traj, W);
   }
   for (int l = 0; l < LANES; ++l) out_acc[l] = L[l].a;
 }

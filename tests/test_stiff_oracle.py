@@ -1,5 +1,5 @@
-"""Pin the stiff methods' C restatement (oracle/rk_ref.c: 'rosenbrock' = the L-stable
-ROS4 method, 'auto' = DOPRI5 + per-walker stiffness test + Rosenbrock restart — the
+"""Pin the stiff methods' C restatement (oracle/rk_ref.c: 'rosenbrock' = the stiffly
+accurate RODAS method, 'auto' = DOPRI5 + per-walker stiffness test + Rosenbrock restart — the
 kernels' algorithm) against the reference's algorithm on stiff draws:
 odeint's LSODA switches to BDF there (Framework.py:656), so the yardstick is a tight
 implicit solution (scipy Radau, rtol 1e-13) and the reference's own odeint."""
@@ -28,25 +28,41 @@ ODEINT_TOL = 1.49012e-8
 
 def _ros_constants():
     src = open(STIFF_H).read()
-    block = src[src.index("namespace ros {"):src.index("constexpr double inv_gam")]
+    block = src[src.index("namespace ros {"):src.index("constexpr double safe")]
     vals = dict((k, float(v)) for k, v in re.findall(r"(\w+) = (-?[0-9.eE+-]+)", block))
     return vals
 
 
-def test_ros4_coefficients_order_and_l_stability():
-    """The shipped ROS4 set (stiff.cuh) satisfies the eight order-4 conditions of a
-    Rosenbrock method, its embedded method the four order-3 ones (Hairer & Wanner II,
-    Table IV.7.1, in the Kaps–Rentrop form of the code), R(∞) ≈ 0 (L-stable) and
-    |R(iy)| ≤ 1 (A-stable); the time-derivative coefficients are Σγ_ij and Σα_ij."""
+def _rodas_tableau():
+    """The shipped RODAS set (stiff.cuh) in matrix form: stage-argument weights A (stage 6
+    = the embedded solution), increment couplings C, solution weights m (y_new = stage-6
+    argument + k6) and embedded weights mh."""
     c = _ros_constants()
-    gam = c["gam"]
-    A = np.zeros((4, 4)); C = np.zeros((4, 4))
-    A[1, 0] = c["a21"]; A[2, 0] = A[3, 0] = c["a31"]; A[2, 1] = A[3, 1] = c["a32"]
-    C[1, 0] = c["c21"]; C[2, 0] = c["c31"]; C[2, 1] = c["c32"]
-    C[3, 0] = c["c41"]; C[3, 1] = c["c42"]; C[3, 2] = c["c43"]
-    m = np.array([c["m1"], c["m2"], c["m3"], c["m4"]]); e = np.array([c["e1"], c["e2"], c["e3"], c["e4"]])
-    Gi = np.diag(np.full(4, 1 / gam)) - C
-    G = np.linalg.inv(Gi)
+    n = 6
+    A = np.zeros((n, n)); C = np.zeros((n, n))
+    for i in range(2, 6):
+        for j in range(1, i):
+            A[i - 1, j - 1] = c[f"a{i}{j}"]
+    A[5, :4] = A[4, :4]; A[5, 4] = 1.0
+    for i in range(2, 7):
+        for j in range(1, i):
+            C[i - 1, j - 1] = c[f"c{i}{j}"]
+    m = np.array([c["a51"], c["a52"], c["a53"], c["a54"], 1.0, 1.0])
+    mh = np.array([c["a51"], c["a52"], c["a53"], c["a54"], 1.0, 0.0])
+    return c, A, C, m, mh
+
+
+def test_rodas_coefficients_order_and_l_stability():
+    """The shipped RODAS set (stiff.cuh) satisfies the eight order-4 conditions of a
+    Rosenbrock method, its embedded method the four order-3 ones (Hairer & Wanner II,
+    §VI.4, in the transformed form of the code); BOTH are L-stable (R(∞) = 0) and
+    A-stable — the embedded estimate being L-stable is what keeps the step size of a
+    stiff walker on its slow manifold large; the stage times are Σα_ij and the ∂f/∂t
+    weights Σγ_ij."""
+    c, A, C, m, mh = _rodas_tableau()
+    gam, n = c["gam"], 6
+    assert c["inv_gam"] == 1.0 / gam
+    G = np.linalg.inv(np.diag(np.full(n, 1 / gam)) - C)
     alpha = A @ G
     beta = np.tril(alpha + G, -1)
     bp, al = beta.sum(1), alpha.sum(1)
@@ -56,16 +72,40 @@ def test_ros4_coefficients_order_and_l_stability():
                          b @ al ** 3 - 1 / 4, (b * al) @ alpha @ bp - (1 / 8 - gam / 3),
                          b @ beta @ al ** 2 - (1 / 12 - gam / 3),
                          b @ beta @ beta @ bp - (1 / 24 - gam / 2 + 1.5 * gam ** 2 - gam ** 3)])
-    assert np.abs(conds(m @ G)).max() < 1e-14
-    assert np.abs(conds((m - e) @ G)[:4]).max() < 1e-14
-    assert np.abs(conds((m - e) @ G)[4:]).max() > 1e-3  # the estimate is genuinely order 3
+    assert np.abs(conds(m @ G)).max() < 1e-13
+    assert np.abs(conds(mh @ G)[:4]).max() < 1e-13
+    assert np.abs(conds(mh @ G)[4:]).max() > 1e-3  # the estimate is genuinely order 3
     B = alpha + G
-    b = m @ G
-    R = lambda z: 1 + z * (b @ np.linalg.solve(np.eye(4) - z * B, np.ones(4)))
-    assert abs(1 - b @ np.linalg.solve(B, np.ones(4))) < 1e-4           # R(∞) ≈ 0
-    assert max(abs(R(1j * y)) for y in np.logspace(-3, 5, 400)) <= 1 + 1e-12
-    np.testing.assert_allclose(al[1:3], [c["a2x"], c["a3x"]], rtol=1e-13)
-    np.testing.assert_allclose(G.sum(1), [c["g1x"], c["g2x"], c["g3x"], c["g4x"]], rtol=1e-13)
+    for w in (m @ G, mh @ G):
+        assert abs(1 - w @ np.linalg.solve(B, np.ones(n))) < 1e-13          # R(∞) = 0
+        R = lambda z: 1 + z * (w @ np.linalg.solve(np.eye(n) - z * B, np.ones(n)))
+        assert max(abs(R(1j * y)) for y in np.logspace(-3, 6, 400)) <= 1 + 1e-12
+    np.testing.assert_allclose(al, [0, c["c2x"], c["c3x"], c["c4x"], 1, 1], atol=1e-14)
+    np.testing.assert_allclose(G.sum(1), [c["d1"], c["d2"], c["d3"], c["d4"], 0, 0], atol=1e-14)
+
+
+def test_rodas_continuous_extension_order():
+    """The dense-output weights h2j, h3j: y(θ) = (1−θ)·y0 + θ·(y1 + (1−θ)·(q3 + θ·q4)) on
+    y' = λy reproduces exp(θz) to third order in z for every θ (the extension's order)."""
+    c, A, C, m, mh = _rodas_tableau()
+    gam, n = c["gam"], 6
+    h2 = np.array([c[f"h2{j}"] for j in range(1, 6)] + [0.0])
+    h3 = np.array([c[f"h3{j}"] for j in range(1, 6)] + [0.0])
+    G = np.linalg.inv(np.diag(np.full(n, 1 / gam)) - C)
+    B = A @ G + G
+
+    def dense(z, th):  # one step of y' = λy from y0 = 1 (z = hλ); increments K = z·(I − zB)^{-1}·G·1…
+        # k_i solves (1/(γh) − λ) k_i = λ(y0 + Σ a_ij k_j) + Σ (c_ij/h) k_j, in units of y0
+        K = np.zeros(n)
+        for i in range(n):
+            rhs = z * (1 + A[i, :i] @ K[:i]) + C[i, :i] @ K[:i]
+            K[i] = rhs / (1 / gam - z)
+        y1 = 1 + m @ K
+        return (1 - th) + th * (y1 + (1 - th) * (h2 @ K + th * (h3 @ K)))
+
+    for th in (0.2, 0.5, 0.9):
+        errs = [abs(dense(z, th) - np.exp(th * z)) for z in (1e-2, 5e-3)]
+        assert errs[0] / errs[1] > 2 ** 3.7, (th, errs)  # local error O(z^4)
 
 
 def test_inv_fourth_root_accuracy():
@@ -152,7 +192,7 @@ def test_auto_chi_at_least_as_accurate_as_reference_odeint():
 
 def test_stiff_walker_in_a_wave_of_nonstiff_ones():
     """One stiff walker among 63 demo draws: it is evicted from the shared DOPRI5 step and
-    redone by ROS4; every walker stays within tolerance of the tight solution, and the
+    redone by RODAS; every walker stays within tolerance of the tight solution, and the
     wave's step count stays that of the non-stiff draws (the stiff lane does not pin it)."""
     m = product_model("two_i")
     fp = m.fit_problem()
