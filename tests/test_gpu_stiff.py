@@ -119,7 +119,7 @@ def test_auto_chi_only_mode_equals_trajectory_mode():
 def test_mh_stiff_methods_vs_c_restatement(method):
     """Philox MH chains where some proposals are stiff: the device chain equals the C
     restatement's (rtol 1e-8 as for DOPRI5 MH: ocml vs libm exp/log in the proposal)."""
-    W = 128 if method == "auto" else 8  # (the C restatement of ROS4 for every chain is slow)
+    W = 128 if method == "auto" else 8  # (the C restatement of RODAS for every chain is slow)
     m = product_model("two_i", method=method)
     theta = _mixed_thetas("two_i", W, [1, 64, 65, 127] if method == "auto" else [1])
     y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
