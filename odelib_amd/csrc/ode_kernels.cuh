@@ -756,8 +756,14 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t G, int32_t c) {
 template <class M>
 constexpr int kPmax = M::P + (M::S < 4 ? M::S : 4);
 
+// S = 5 stiff methods: the DOPRI5 + RODAS kernel needs 256 VGPRs + 14-22 AGPRs (one wave
+// per SIMD); asking for two leaves 32-48 B of scratch and measured (262 144 walkers,
+// profiles/r02o_occ*): `auto` 1.25 vs 1.70 ms without trajectory, 2.09 vs 2.22 with,
+// `rosenbrock` 6.3 vs 8.3 ms.  S = 6..8 kernels sit at one wave per SIMD for DOPRI5 too.
 template <class M, int METHOD, bool TRAJ, bool NT>
-__global__ void __launch_bounds__(256) k_integrate(const DevProblem pb, const IntegrateArgs ia) {
+__global__ void __launch_bounds__(256)
+    __attribute__((amdgpu_waves_per_eu((METHOD >= kAuto && M::S == 5) ? 2 : 1)))
+    k_integrate(const DevProblem pb, const IntegrateArgs ia) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
   const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x, ia.xcd_remap) : (int64_t)blockIdx.x;
