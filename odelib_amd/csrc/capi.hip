@@ -385,7 +385,7 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   // RK4 per-interval constants: h = (t_i - t_{i-1}) / n, h/2, h/6, t_{i-1}
   // (IEEE-correctly-rounded on host and device alike, so the table is exact)
   const int nsub = p->method == OE_METHOD_RK4 ? p->rk4_substeps : 1;
-  std::vector<double> rk4(4 * (size_t)(p->n_times - 1));
+  std::vector<double> rk4(4 * (size_t)p->n_times);  // + one padding row (the kernel's look-ahead)
   for (int i = 1; i < p->n_times; ++i) {
     const double h = (p->times[i] - p->times[i - 1]) / (double)nsub;
     rk4[4 * (i - 1)] = h;
@@ -393,6 +393,7 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
     rk4[4 * (i - 1) + 2] = h / 6.0;
     rk4[4 * (i - 1) + 3] = p->times[i - 1];
   }
+  for (int j = 0; j < 4; ++j) rk4[4 * (size_t)(p->n_times - 1) + j] = rk4[4 * (size_t)(p->n_times - 2) + j];
 
   // (re)upload
   OE_HIP(c, hipStreamSynchronize(c->stream));
@@ -401,8 +402,12 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   if (c->d_rk4) { OE_HIP(c, hipFree(c->d_rk4)); c->d_rk4 = nullptr; }
   OE_HIP(c, hipMalloc(&c->d_rk4, sizeof(double) * rk4.size()));
   OE_HIP(c, hipMemcpy(c->d_rk4, rk4.data(), sizeof(double) * rk4.size(), hipMemcpyHostToDevice));
-  OE_HIP(c, hipMalloc(&c->d_times, sizeof(double) * p->n_times));
-  OE_HIP(c, hipMemcpy(c->d_times, p->times, sizeof(double) * p->n_times, hipMemcpyHostToDevice));
+  // the grid plus a +inf sentinel at index T: the DOPRI5 dense-output loop reads the
+  // next grid time one point ahead without clamping the index
+  std::vector<double> tg(p->times, p->times + p->n_times);
+  tg.push_back(HUGE_VAL);
+  OE_HIP(c, hipMalloc(&c->d_times, sizeof(double) * tg.size()));
+  OE_HIP(c, hipMemcpy(c->d_times, tg.data(), sizeof(double) * tg.size(), hipMemcpyHostToDevice));
   if (p->n_obs > 0) {
     OE_HIP(c, hipMalloc(&c->d_obs, sizeof(Obs) * p->n_obs));
     OE_HIP(c, hipMemcpy(c->d_obs, obs.data(), sizeof(Obs) * p->n_obs, hipMemcpyHostToDevice));

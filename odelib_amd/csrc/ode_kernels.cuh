@@ -42,8 +42,8 @@ __device__ __forceinline__ cptr<T> kconst(const T* p) {
 }
 
 struct DevProblem {
-  const double* times;  // [T]
-  const double* rk4;    // [T-1][4]: h, h/2, h/6, t_i  (host-computed per interval)
+  const double* times;  // [T + 1]: the grid, then a +inf sentinel
+  const double* rk4;    // [T][4]: h, h/2, h/6, t_i per interval (host-computed); row T-1 repeats row T-2
   const Obs* obs;       // [n_obs]
   int32_t T;
   int32_t n_obs;
@@ -194,22 +194,45 @@ __device__ __forceinline__ void check_finite(const double (&y)[S], Acc& a) {
 // Store grid row i of the trajectory (TRAJ) and track the minimum state.  `off` is
 // the lane's byte offset w*8 (32-bit); rows are stored through a per-row buffer
 // descriptor (S*W*8 < 2^32, checked on the host): no per-store VALU address math.
+template <int S>
+__device__ __forceinline__ void track_min(const double (&y)[S], Acc& a) {
+  // raw v_min_f64 (fmin's canonicalising copies of both operands doubled the VALU count
+  // of the minimum); a quiet NaN operand returns the other, as C fmin does.  Pairwise
+  // over the states (min is exact, so the order cannot change the result), then one
+  // min into the running value: a shorter dependency chain than a serial fold.
+  if constexpr (S == 1) {
+    a.ymin = min_raw(a.ymin, y[0]);
+  } else {
+    double m[(S + 1) / 2];
+#pragma unroll
+    for (int j = 0; j < S / 2; ++j) m[j] = min_raw(y[2 * j], y[2 * j + 1]);
+    if constexpr (S % 2) m[S / 2] = y[S - 1];
+    double r = m[0];
+#pragma unroll
+    for (int j = 1; j < (S + 1) / 2; ++j) r = min_raw(r, m[j]);
+    a.ymin = min_raw(a.ymin, r);
+  }
+}
+
+// Store one trajectory row whose first element is at `row` (= traj + i*S*W).
 template <int S, bool TRAJ, bool NT>
-__device__ __forceinline__ void store_row(int i, const double (&y)[S], double* __restrict__ traj,
-                                          int64_t W, uint32_t off, bool active, Acc& a) {
+__device__ __forceinline__ void store_row_at(double* row, const double (&y)[S], int64_t W, uint32_t off,
+                                             bool active, Acc& a) {
+  track_min<S>(y, a);  // first: it schedules among the producer's VALU, not after the stores
   if constexpr (TRAJ) {
     if (active) {
       const uint32_t row_bytes = (uint32_t)(S * W * 8);
-      const __amdgpu_buffer_rsrc_t rsrc =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(traj + (int64_t)i * S * W), 0, row_bytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, row_bytes, 0x00020000);
 #pragma unroll
       for (int s = 0; s < S; ++s) st_row<NT>(rsrc, off, (uint32_t)(s * W * 8), y[s]);
     }
   }
-  // raw v_min_f64 (fmin's canonicalising copies of both operands doubled the VALU count
-  // of the minimum); a quiet NaN operand returns the other, as C fmin does
-#pragma unroll
-  for (int s = 0; s < S; ++s) a.ymin = min_raw(a.ymin, y[s]);
+}
+
+template <int S, bool TRAJ, bool NT>
+__device__ __forceinline__ void store_row(int i, const double (&y)[S], double* __restrict__ traj,
+                                          int64_t W, uint32_t off, bool active, Acc& a) {
+  store_row_at<S, TRAJ, NT>(TRAJ ? traj + (int64_t)i * S * W : nullptr, y, W, off, active, a);
 }
 
 // Fold every observation recorded at grid index i into the likelihood (caller knows
@@ -295,20 +318,25 @@ template <class M, int PMAX, bool TRAJ, bool NT>
 __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[M::S],
                                               const double (&p)[PMAX], double* traj,
                                               int64_t W, uint32_t off, bool active, Acc& a) {
+  constexpr int S = M::S;
   int k = 0;
-  emit<M::S, TRAJ, NT, TRAJ>(pb, 0, y, traj, W, off, active, k, a);
+  emit<S, TRAJ, NT, TRAJ>(pb, 0, y, traj, W, off, active, k, a);
   const int n = pb.substeps;
-  const cptr<double> tab = kconst(pb.rk4);
   const cptr<Obs> obs = kconst(pb.obs);
   // Per-interval constants computed on the host exactly as h = (t_i - t_{i-1}) / n,
   // hh = 0.5*h, h6 = h/6, t_{i-1}; substep j starts at t_{i-1} + j*h.  The NEXT
   // interval's row is loaded while this interval computes: a lone wave otherwise waits
-  // out a scalar-cache miss (one 64-B line per two intervals) every other step.
+  // out a scalar-cache miss (one 64-B line per two intervals) every other step.  The
+  // table has a padding row at the end, so the look-ahead pointer needs no clamp, and
+  // the trajectory row pointer advances with the grid index (no per-row multiply: a
+  // lone wave issues scalar instructions one per slot, like VALU).
+  cptr<double> tab = kconst(pb.rk4);
   double h = tab[0], hh = tab[1], h6 = tab[2], t = tab[3];
-  const int last_row = pb.T - 2;
-  auto interval = [&](int i) {
-    const int nx = i < last_row ? i : last_row;  // table row of interval i+1 (clamped)
-    const double hn = tab[4 * nx], hhn = tab[4 * nx + 1], h6n = tab[4 * nx + 2], tn = tab[4 * nx + 3];
+  tab += 4;
+  double* trow = TRAJ ? traj + (int64_t)S * W : nullptr;
+  auto interval = [&]() {
+    const double hn = tab[0], hhn = tab[1], h6n = tab[2], tn = tab[3];
+    tab += 4;
     for (int j = 0; j < n; ++j) rk4_step<M, PMAX>(y, t + (double)j * h, h, hh, h6, p);
     h = hn; hh = hhn; h6 = h6n; t = tn;
   };
@@ -317,12 +345,19 @@ __device__ __forceinline__ void integrate_rk4(const DevProblem& pb, double (&y)[
     // observation-free segment [i, next): step + row store only (no per-step obs logic)
     const int next = (k < pb.n_obs) ? obs[k].tidx : pb.T;
     for (; i < next; ++i) {
-      interval(i);
-      if constexpr (TRAJ) store_row<M::S, TRAJ, NT>(i, y, traj, W, off, active, a);
+      interval();
+      if constexpr (TRAJ) {
+        store_row_at<S, TRAJ, NT>(trow, y, W, off, active, a);
+        trow += S * W;
+      }
     }
     if (i < pb.T) {  // i == next: an observed grid point
-      interval(i);
-      emit<M::S, TRAJ, NT, TRAJ>(pb, i, y, traj, W, off, active, k, a);
+      interval();
+      if constexpr (TRAJ) {
+        store_row_at<S, TRAJ, NT>(trow, y, W, off, active, a);
+        trow += S * W;
+      }
+      observe<S, TRAJ>(pb, i, y, k, a);
       ++i;
     }
   }
@@ -404,6 +439,42 @@ __device__ __forceinline__ double inv_fifth_root(double x) {
                  : r == 3 ? 0.6597539553864471 : 0.5743491774985174;
   return ldexp(c * y, -q);
 }
+
+// inv_fifth_root of a WAVE-UNIFORM x (the step controller's err): the exponent part
+// 2^(-r/5)·2^(-q) comes from one scalar load of kFifthScale[e + kFifthBias] instead of
+// the integer division, the 5-way select and the ldexp (~30 scalar instructions, which a
+// lone wave issues one per slot like VALU).  kFifthScale[e] = c_r·2^(-q) is exact (a
+// power-of-two scaling of a normal number) and c_r·y ∈ (0.5, 1.3), so (c_r·2^(-q))·y is
+// the same double as ldexp(c_r·y, -q): bit-identical to inv_fifth_root.
+constexpr int kFifthBias = 1088;  // frexp exponents of finite positive doubles: -1073 .. 1024
+struct FifthScale {
+  double v[2 * kFifthBias];
+  constexpr FifthScale() : v() {
+    const double c[5] = {1.0, 0.8705505632961241, 0.757858283255199, 0.6597539553864471, 0.5743491774985174};
+    for (int j = 0; j < 2 * kFifthBias; ++j) {
+      const int e = j - kFifthBias;
+      int q = e / 5, r = e % 5;
+      if (r < 0) { r += 5; q -= 1; }
+      const int be = 1023 - q;  // 2^(-q), a normal double for every e above
+      v[j] = (be > 0 && be < 2047) ? c[r] * __builtin_bit_cast(double, (unsigned long long)be << 52) : 0.0;
+    }
+  }
+};
+__device__ const FifthScale kFifthScale{};
+__device__ __forceinline__ double inv_fifth_root_uniform(double x, cptr<double> scale) {
+  int e;
+  const double m = frexp(x, &e);
+  e = __builtin_amdgcn_readfirstlane(e);
+  const double sc = scale[e + kFifthBias];
+  double y = fma(fma(0.2395, m, -0.6505), m, 1.4123);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double y2 = y * y;
+    const double y5 = (y2 * y2) * y;
+    y = (y * fma(-m, y5, 6.0)) * 0.2;
+  }
+  return sc * y;
+}
 }  // namespace dp
 
 // AUTO: Hairer's stiffness test on every accepted step (h·|λ| estimated from the last two
@@ -465,6 +536,10 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
   constexpr bool kLean = S > 8;
   int i = 1;
   double t_i = times[1];
+  cptr<double> tnext = times + 2;  // &times[i + 1]
+  // row i of the trajectory, advanced with i (no 64-bit multiply per emitted row)
+  double* trow = TRAJ ? traj + (int64_t)S * W : nullptr;
+  const cptr<double> fifth = kconst(kFifthScale.v);
   int nxt = (k < pb.n_obs) ? kconst(pb.obs)[k].tidx : 0x7fffffff;  // next observed index
   double t_obs = (nxt < pb.T) ? times[nxt] : __builtin_inf();        // and its time
   int nst = 0;  // steps since the last grid point
@@ -573,9 +648,11 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
         // grid points strictly inside the step: dense output (no per-point test for the
         // end point, whose row is the new state itself: handled after the loop, so the
         // dense values go straight to the store registers)
-        while (i < pb.T && t_i < tn) {
+        // (times[T] is a +inf sentinel: the look-ahead load needs no clamp, and t_i < tn
+        //  fails once i reaches T)
+        while (t_i < tn) {
           const double ti = t_i;
-          t_i = times[i + 1 < pb.T ? i + 1 : i];  // issued now, used next iteration
+          t_i = *tnext++;  // times[i + 1]: issued now, used next iteration
           if (TRAJ || i == nxt) {
             const double th = (ti - t) * rh;
             const double th1 = 1.0 - th;
@@ -584,25 +661,27 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
             for (int s = 0; s < S; ++s)
               yo[s] = fma(th, fma(th1, fma(th, fma(th1, r5[s], r4[s]), bsp[s]), ydf[s]), y[s]);
             // (an evicted lane's state is NaN, so its dense output is NaN already)
-            store_row<S, TRAJ, NT>(i, yo, traj, W, off, active, a);
+            store_row_at<S, TRAJ, NT>(trow, yo, W, off, active, a);
             if (i == nxt) {
               observe_next<S>(pb, i, yo, k, nxt, a);
-              t_obs = (nxt < pb.T) ? times[nxt] : __builtin_inf();
+              t_obs = times[nxt < pb.T ? nxt : pb.T];
             }
           }
           ++i;
+          if constexpr (TRAJ) trow += S * W;
           nst = 0;
         }
-        if (i < pb.T && t_i == tn) {  // a grid point on the step's end
-          t_i = times[i + 1 < pb.T ? i + 1 : i];
+        if (t_i == tn) {  // a grid point on the step's end
+          t_i = *tnext++;
           if (TRAJ || i == nxt) {
-            store_row<S, TRAJ, NT>(i, yn, traj, W, off, active, a);
+            store_row_at<S, TRAJ, NT>(trow, yn, W, off, active, a);
             if (i == nxt) {
               observe_next<S>(pb, i, yn, k, nxt, a);
-              t_obs = (nxt < pb.T) ? times[nxt] : __builtin_inf();
+              t_obs = times[nxt < pb.T ? nxt : pb.T];
             }
           }
           ++i;
+          if constexpr (TRAJ) trow += S * W;
           nst = 0;
         }
       } else {
@@ -644,13 +723,13 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
       for (int s = 0; s < S; ++s) { y[s] = yn[s]; k1[s] = k7[s]; }
       t = tn;
-      double fac = (err > 0.0) ? safe * inv_fifth_root(err) : facmax;
+      double fac = (err > 0.0) ? safe * inv_fifth_root_uniform(err, fifth) : facmax;
       fac = fmin(facmax, fmax(facmin, fac));
       if (last_rej) fac = fmin(fac, 1.0);
       h = h * fac;
       last_rej = false;
     } else {
-      h = h * fmax(facmin, safe * inv_fifth_root(err));
+      h = h * fmax(facmin, safe * inv_fifth_root_uniform(err, fifth));
       last_rej = true;
     }
     // ---- budget: evict the walkers that pin the wave's step ----
