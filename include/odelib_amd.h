@@ -61,10 +61,11 @@ enum {
                            dense output onto the times grid */
   OE_METHOD_AUTO = 2,   /* odeint's LSODA behaviour (Framework.py:656): DOPRI5 with a per-walker
                            stiffness test; stiff or over-budget walkers are integrated again by
-                           the Rosenbrock method (status bit OE_STATUS_STIFF).  n_states <= 8 */
+                           the Rosenbrock method (status bit OE_STATUS_STIFF).  n_states <= 32
+                           (above 8 the Jacobian and LU factors live in private memory) */
   OE_METHOD_ROSENBROCK = 3 /* stiffly accurate Rosenbrock 4(3) (RODAS) for every walker, exact
                               Jacobian by dual numbers, continuous extension onto the output
-                              times.  n_states <= 8 */
+                              times.  n_states <= 32 */
 };
 
 /* built-in right-hand sides (demo notebook models + synthetic chain) */

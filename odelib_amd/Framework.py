@@ -8,7 +8,9 @@ ODE callable is bound to a compiled device RHS by ``models.resolve``.
 
 Engine options (keyword-only, new): ``method`` ('auto' default — like odeint's LSODA:
 adaptive DOPRI5 with a per-walker stiffness test, stiff walkers redone by an L-stable
-Rosenbrock method; 'dopri5' where that is unavailable — or 'dopri5', 'rosenbrock', 'rk4'), ``rtol``/``atol`` (odeint defaults), ``rk4_substeps``,
+Rosenbrock method; 'dopri5' by default for models wider than 8 states or where the
+stiff methods are unavailable — or 'dopri5', 'rosenbrock', 'rk4'), ``rtol``/``atol``
+(odeint defaults), ``rk4_substeps``,
 ``max_steps`` (odeint's mxstep), ``device`` (HIP device index; default: torch's current
 device when the engine is built), ``device_model``
 (force a built-in RHS, or 'rtc'), ``device_rhs`` (C++ body of the RHS for hipRTC).
@@ -121,7 +123,8 @@ class ModelFramework:
         eng = {k: kwargs.pop(k) for k in list(kwargs) if k in _ENGINE_KW
                and k not in self._pnames and k not in self._snames}
         # default 'auto': odeint's LSODA behaviour (non-stiff DOPRI5, stiff walkers by the
-        # Rosenbrock method); 'dopri5' where the stiff methods are unavailable
+        # Rosenbrock method); 'dopri5' for wide models or where the stiff methods are
+        # unavailable (engine.AUTO_DEFAULT_MAX_STATES)
         self.method = eng.get("method", "auto")
         self._method_default = "method" not in eng
         self.rtol = float(eng.get("rtol", ODEINT_TOL))

@@ -47,7 +47,7 @@ EXPORTED = (
 
 class NativeUnsupported(RuntimeError):
     """OE_ERR_UNSUPPORTED: the model / method combination is not available (e.g. a stiff
-    method for n_states > 8, or for a C body that does not compile for dual numbers)."""
+    method for n_states > 32, or for a C body that does not compile for dual numbers)."""
 
 
 class NativeUnavailable(RuntimeError):

@@ -60,7 +60,8 @@ enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8
 // integrators (OE_METHOD_*): fixed-step RK4, DOPRI5, DOPRI5 with stiffness detection and
 // the Rosenbrock fallback for stiff / over-budget walkers (LSODA-like), Rosenbrock only
 enum : int { kRK4 = 0, kDOPRI5 = 1, kAuto = 2, kRosenbrock = 3 };
-constexpr int kStiffMaxS = 8;  // the stiff methods factor an S x S matrix per lane in registers
+constexpr int kStiffRegS = 8;   // up to here the stiff methods factor the S x S matrix in registers,
+constexpr int kStiffMaxS = 32;  // above it in private memory (stiff.cuh); wider models: DOPRI5 only
 constexpr int kStiffTestSteps = 3;  // auto: stiffness test from the 3rd step within one output interval
 
 // per-lane accumulators of the fused likelihood
@@ -146,6 +147,11 @@ __device__ __forceinline__ double wave_min(double v) {
   v = fmin(v, dpp_f64<0x143, 0xC>(v));
   return lane63(v);
 }
+
+template <bool B, class T, class F>
+struct pick_type { using type = T; };
+template <class T, class F>
+struct pick_type<false, T, F> { using type = F; };
 
 // register-array element at a (uniform) runtime index without spilling the array
 // to scratch: a compile-time-unrolled select chain
@@ -575,6 +581,20 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
 #pragma unroll
     for (int s = 0; s < S; ++s)
       yn[s] = fma(b76, k6[s], fma(b75, k5[s], fma(b74, k4[s], fma(b73, k3[s], fma(b71, k1[s], y[s])))));
+    // AUTO, wide models: the stiffness test's Σ(ynew − y6)² is summed here, on the steps
+    // that will test (the same wave-uniform gate, one step ahead of the ++nst below), so
+    // the stage-6 input dies before k7 instead of living through the error norm — S more
+    // doubles at the kernel's register peak (same values, same order: bit-identical)
+    double stden_early = 0.0;
+    if constexpr (AUTO && kLean) {
+      if (nst + 1 >= kStiffTestSteps) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const double dy = yn[s] - yt[s];
+          stden_early = fma(dy, dy, stden_early);
+        }
+      }
+    }
     M::rhs(yn, t + h, p, k7);
     // ---- per-lane max-norm error: argmax of |e_s|/sk_s by exact cross-multiplication,
     //      then ONE division; non-finite anywhere -> 1e30 (forces a reject) ----
@@ -602,12 +622,15 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
       // wave-uniform gate): a stiff lane pins the shared step far below the grid spacing,
       // while a non-stiff wave spans grid points with nearly every step and never pays.
       if (AUTO && nst >= kStiffTestSteps) {
-        double stnum = 0.0, stden = 0.0;
+        double stnum = 0.0, stden = stden_early;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          const double dk = k7[s] - k6[s], dy = yn[s] - yt[s];
+          const double dk = k7[s] - k6[s];
           stnum = fma(dk, dk, stnum);
-          stden = fma(dy, dy, stden);
+          if constexpr (!kLean) {
+            const double dy = yn[s] - yt[s];
+            stden = fma(dy, dy, stden);
+          }
         }
         if (stden > 0.0 && (h * h) * stnum > 10.5625 * stden) {
           n_nonstiff = 0;
@@ -780,7 +803,10 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
     // step budget) are integrated again from their initial state by the Rosenbrock
     // method, their likelihood accumulated afresh (status bit ST_STIFF)
     constexpr int S = M::S;
-    double yi[S];
+    // the initial state for a restart; wide models keep it in private memory rather than
+    // in S register pairs live across the whole DOPRI5 pass
+    using YI = typename pick_type<(S <= kStiffRegS), double, volatile double>::type;
+    YI yi[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) yi[s] = y[s];
     const bool redo = integrate_dopri5<M, PMAX, TRAJ, NT, true>(pb, y, p, traj, W, off, active, a);
@@ -791,10 +817,10 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
         a = acc_init();
         a.status = ST_STIFF;
       }
-      integrate_rosenbrock<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, redo, a);
+      rosenbrock_lanes<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, redo, a);
     }
   } else {  // kRosenbrock: the Rosenbrock method for every walker
-    integrate_rosenbrock<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, active, a);
+    rosenbrock_lanes<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, active, a);
   }
 }
 

@@ -495,4 +495,324 @@ __device__ __forceinline__ void integrate_rosenbrock(const DevProblem& pb, doubl
   if (part) check_finite(y, a);
 }
 
+
+// ---- S > kStiffRegS: the same RODAS integration with its matrices in private memory ----
+// (1/(γh))·I − J at S = 20 is 400 doubles per lane, and J another 400: beyond the VGPR
+// file, so the wide models keep J, the LU factors and the stage vectors in private
+// (scratch) memory, indexed at run time in non-unrolled loops — the rare stiff walkers of
+// a wide model pay memory traffic instead of every kernel paying registers.  The
+// arithmetic is the register version's, operation for operation (the row interchanges
+// move rows instead of selecting, the same data movement), so the C restatement covers
+// both.  The Jacobian is taken column by column with one-tangent dual numbers: each
+// tangent of Dual<S+1> is computed by the same operations whatever the other tangents
+// hold, so every entry is bitwise the one the (S+1)-tangent evaluation gives.
+template <class M, int PMAX>
+__device__ __forceinline__ void jac_eval_cols(const double (&y)[M::S], double t, const double (&p)[PMAX],
+                                              double (&f)[M::S], double (&J)[M::S * M::S], double (&ft)[M::S]) {
+  constexpr int S = M::S;
+  using D = Dual<1>;
+#pragma unroll 1
+  for (int j = 0; j <= S; ++j) {
+    D yd[S], pd[PMAX], fd[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) { yd[s] = D(y[s]); yd[s].d[0] = (s == j) ? 1.0 : 0.0; }
+    D td(t);
+    td.d[0] = (j == S) ? 1.0 : 0.0;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) pd[q] = D(p[q]);
+    M::rhs(yd, td, pd, fd);
+    if (j < S) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) J[s * S + j] = fd[s].d[0];
+    } else {
+#pragma unroll
+      for (int s = 0; s < S; ++s) { ft[s] = fd[s].d[0]; f[s] = fd[s].v; }
+    }
+  }
+}
+
+namespace ros {
+template <int S>
+__device__ __forceinline__ bool lu_factor_big(double (&a)[S * S], int (&piv)[S], double (&dinv)[S]) {
+  bool any_swap = false;
+#pragma unroll 1
+  for (int k = 0; k < S; ++k) {
+    piv[k] = k;
+    if (k + 1 < S) {
+      double colmax = 0.0;
+#pragma unroll 1
+      for (int i = k + 1; i < S; ++i) colmax = fmax(colmax, fabs(a[i * S + k]));
+      const bool need = fabs(a[k * S + k]) < kPivotThreshold * colmax;
+      if (__ballot(need) != 0ull) {
+        any_swap = true;
+        int pk = k;
+        double best = fabs(a[k * S + k]);
+#pragma unroll 1
+        for (int i = k + 1; i < S; ++i) {
+          const double v = fabs(a[i * S + k]);
+          if (v > best) { best = v; pk = i; }
+        }
+        if (!need) pk = k;
+        piv[k] = pk;
+        if (pk != k) {
+#pragma unroll 1
+          for (int j = 0; j < S; ++j) {
+            const double ak = a[k * S + j];
+            a[k * S + j] = a[pk * S + j];
+            a[pk * S + j] = ak;
+          }
+        }
+      }
+    }
+    const double inv = 1.0 / a[k * S + k];
+    dinv[k] = inv;
+#pragma unroll 1
+    for (int i = k + 1; i < S; ++i) {
+      const double l = a[i * S + k] * inv;
+      a[i * S + k] = l;
+#pragma unroll 1
+      for (int j = k + 1; j < S; ++j) a[i * S + j] = fma(-l, a[k * S + j], a[i * S + j]);
+    }
+  }
+  return any_swap;
+}
+
+template <int S>
+__device__ __forceinline__ void lu_solve_big(const double (&a)[S * S], const int (&piv)[S], const double (&dinv)[S],
+                                             bool any_swap, double (&b)[S]) {
+  if (any_swap) {
+#pragma unroll 1
+    for (int k = 0; k < S; ++k) {
+      const int pk = piv[k];
+      if (pk != k) {
+        const double bk = b[k];
+        b[k] = b[pk];
+        b[pk] = bk;
+      }
+    }
+  }
+#pragma unroll 1
+  for (int k = 0; k < S; ++k) {
+    const double bk = b[k];
+#pragma unroll 1
+    for (int i = k + 1; i < S; ++i) b[i] = fma(-a[i * S + k], bk, b[i]);
+  }
+#pragma unroll 1
+  for (int k = S - 1; k >= 0; --k) {
+    double x = b[k];
+#pragma unroll 1
+    for (int j = k + 1; j < S; ++j) x = fma(-a[k * S + j], b[j], x);
+    b[k] = x * dinv[k];
+  }
+}
+}  // namespace ros
+
+// Called on copies of the caller's state, parameters and accumulators: the run-time
+// indexed arrays live in private memory, the caller's own stay in registers.  (Out of
+// line it measured slower in MH: chain10 'auto' 2.44 vs 2.09 ms per iteration at 262 144
+// walkers; profiles/r02zh_*.)
+template <class M, int PMAX, bool TRAJ, bool NT>
+__device__ __forceinline__ void integrate_rosenbrock_big(const DevProblem& pb, double (&y)[M::S], const double (&p)[PMAX],
+                                                      double* traj, int64_t W, uint32_t off, bool active, bool part,
+                                                      Acc& a) {
+  using namespace ros;
+  constexpr int S = M::S;
+  const cptr<double> times = kconst(pb.times);
+  const double t0 = times[0], tend = times[pb.T - 1];
+  const double rtol = pb.rtol, atol = pb.atol;
+  const bool emit_ok = active && part;
+  bool dead = !part;
+  int k = 0;
+  if (part) emit<S, TRAJ, NT>(pb, 0, y, traj, W, off, emit_ok, k, a);
+  double t = t0;
+  double f0[S], J[S * S], ft[S];
+  jac_eval_cols<M, PMAX>(y, t, p, f0, J, ft);
+
+  double h;
+  {
+    double d0 = 0.0, d1v = 0.0;
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) {
+      const double sk = atol + rtol * fabs(y[s]);
+      d0 = fmax(d0, fabs(y[s]) / sk);
+      d1v = fmax(d1v, fabs(f0[s]) / sk);
+    }
+    double h0 = (d0 <= 1e-5 || d1v <= 1e-5) ? 1e-6 : 0.01 * (d0 / d1v);
+    h0 = fmin(h0, tend - t0);
+    double yt[S], f1[S];
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) yt[s] = fma(h0, f0[s], y[s]);
+    M::rhs(yt, t + h0, p, f1);
+    double d2 = 0.0;
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) {
+      const double sk = atol + rtol * fabs(y[s]);
+      d2 = fmax(d2, fabs(f1[s] - f0[s]) / sk);
+    }
+    d2 = d2 / h0;
+    const double dm = fmax(d1v, d2);
+    const double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : inv_fourth_root(dm / 0.01);
+    double hl = fmin(100.0 * h0, h1);
+    if (dead || !__builtin_isfinite(hl) || !(hl > 0.0)) hl = tend - t0;
+    h = wave_min(hl);
+    h = fmin(h, tend - t0);
+  }
+  const double span = tend - t0;
+  const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
+  const int budget = kRosBudget * pb.max_steps;
+  int i = 1, nst = 0;
+  bool last_rej = false;
+  double lu[S * S], dinv[S];
+  int piv[S];
+  double k1[S], k2[S], k3[S], k4[S], k5[S], k6[S], yt[S], fv[S], y1[S];
+  while (i < pb.T) {
+    bool last = false;
+    if (t + h >= tend) { h = tend - t; last = true; }
+    const double rh = 1.0 / h;
+    const double gh = rh * inv_gam;
+    const double c21h = c21 * rh, c31h = c31 * rh, c32h = c32 * rh, c41h = c41 * rh, c42h = c42 * rh,
+                 c43h = c43 * rh, c51h = c51 * rh, c52h = c52 * rh, c53h = c53 * rh, c54h = c54 * rh,
+                 c61h = c61 * rh, c62h = c62 * rh, c63h = c63 * rh, c64h = c64 * rh, c65h = c65 * rh;
+    const double hd1 = h * d1, hd2 = h * d2, hd3 = h * d3, hd4 = h * d4;
+#pragma unroll 1
+    for (int r = 0; r < S; ++r)
+#pragma unroll 1
+      for (int c = 0; c < S; ++c) lu[r * S + c] = (r == c) ? gh - J[r * S + c] : -J[r * S + c];
+    const bool any_swap = lu_factor_big<S>(lu, piv, dinv);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) k1[s] = fma(hd1, ft[s], f0[s]);
+    lu_solve_big<S>(lu, piv, dinv, any_swap, k1);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) yt[s] = fma(a21, k1[s], y[s]);
+    M::rhs(yt, t + c2x * h, p, fv);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) k2[s] = fma(hd2, ft[s], fma(c21h, k1[s], fv[s]));
+    lu_solve_big<S>(lu, piv, dinv, any_swap, k2);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) yt[s] = fma(a32, k2[s], fma(a31, k1[s], y[s]));
+    M::rhs(yt, t + c3x * h, p, fv);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) k3[s] = fma(hd3, ft[s], fma(c32h, k2[s], fma(c31h, k1[s], fv[s])));
+    lu_solve_big<S>(lu, piv, dinv, any_swap, k3);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) yt[s] = fma(a43, k3[s], fma(a42, k2[s], fma(a41, k1[s], y[s])));
+    M::rhs(yt, t + c4x * h, p, fv);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) k4[s] = fma(hd4, ft[s], fma(c43h, k3[s], fma(c42h, k2[s], fma(c41h, k1[s], fv[s]))));
+    lu_solve_big<S>(lu, piv, dinv, any_swap, k4);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) yt[s] = fma(a54, k4[s], fma(a53, k3[s], fma(a52, k2[s], fma(a51, k1[s], y[s]))));
+    M::rhs(yt, t + h, p, fv);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) k5[s] = fma(c54h, k4[s], fma(c53h, k3[s], fma(c52h, k2[s], fma(c51h, k1[s], fv[s]))));
+    lu_solve_big<S>(lu, piv, dinv, any_swap, k5);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) yt[s] = yt[s] + k5[s];  // the embedded solution
+    M::rhs(yt, t + h, p, fv);
+#pragma unroll 1
+    for (int s = 0; s < S; ++s)
+      k6[s] = fma(c65h, k5[s], fma(c64h, k4[s], fma(c63h, k3[s], fma(c62h, k2[s], fma(c61h, k1[s], fv[s])))));
+    lu_solve_big<S>(lu, piv, dinv, any_swap, k6);
+    double num = 0.0, den = 1.0, nfe = 0.0;
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) {
+      y1[s] = yt[s] + k6[s];
+      const double ae = fabs(k6[s]);
+      const double sk = fma(rtol, max_abs_raw(y[s], y1[s]), atol);
+      nfe = fma(ae, 0.0, nfe);
+      nfe = fma(y1[s], 0.0, nfe);
+      if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
+    }
+    double el = num / den;
+    if (!__builtin_isfinite(el) || __builtin_isnan(nfe)) el = 1e30;
+    if (dead) el = 0.0;
+    const double err = wave_max(el);
+    ++nst;
+    if (err <= 1.0) {
+      const double tn = last ? tend : t + h;
+      if (i < pb.T && times[i] < tn) {  // wave-uniform: a grid point inside the step
+        // q3, q4 of the continuous extension, kept in k2 and k3 (not needed any more)
+#pragma unroll 1
+        for (int s = 0; s < S; ++s) {
+          const double q3 = fma(h25, k5[s], fma(h24, k4[s], fma(h23, k3[s], fma(h22, k2[s], h21 * k1[s]))));
+          const double q4 = fma(h35, k5[s], fma(h34, k4[s], fma(h33, k3[s], fma(h32, k2[s], h31 * k1[s]))));
+          k2[s] = q3;
+          k3[s] = q4;
+        }
+        while (i < pb.T && times[i] < tn) {
+          if (part && grid_needs_emit<S, TRAJ>(pb, i, k)) {
+            const double th = (times[i] - t) * rh;
+            const double th1 = 1.0 - th;
+            double yo[S];
+#pragma unroll 1
+            for (int s = 0; s < S; ++s) yo[s] = fma(th, fma(th1, fma(th, k3[s], k2[s]), y1[s]), th1 * y[s]);
+            emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, emit_ok, k, a);
+          }
+          ++i;
+          nst = 0;
+        }
+      }
+#pragma unroll 1
+      for (int s = 0; s < S; ++s) y[s] = part ? y1[s] : y[s];  // bystanders keep their state
+      t = tn;
+      if (i < pb.T && times[i] == tn) {  // a grid point on the step's end
+        if (part && grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, y, traj, W, off, emit_ok, k, a);
+        ++i;
+        nst = 0;
+      }
+      if (i < pb.T) jac_eval_cols<M, PMAX>(y, t, p, f0, J, ft);
+      double fac = (err > 0.0) ? safe * inv_fourth_root(err) : facmax;
+      fac = fmin(facmax, fmax(facmin, fac));
+      if (last_rej) fac = fmin(fac, 1.0);
+      h = h * fac;
+      last_rej = false;
+    } else {
+      h = h * fmax(facmin, safe * inv_fourth_root(err));
+      last_rej = true;
+    }
+    if (nst >= budget || h < hmin) {
+      if (!dead && el >= 0.5 * err) {
+        dead = true;
+        a.status |= ST_MAXSTEP;
+#pragma unroll 1
+        for (int s = 0; s < S; ++s) y[s] = __builtin_nan("");
+      }
+      nst = budget / 2;
+      if (__ballot(!dead) == 0ull) {
+        double yo[S];
+#pragma unroll 1
+        for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
+        for (; i < pb.T; ++i)
+          if (part && grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, emit_ok, k, a);
+        break;
+      }
+      if (h < hmin) h = fmin(1e-3 * span, tend - t);
+    }
+  }
+  if (part) check_finite(y, a);
+}
+
+// Rosenbrock integration of the `part` lanes: registers for S <= kStiffRegS, private
+// memory above (on copies, see integrate_rosenbrock_big).
+template <class M, int PMAX, bool TRAJ, bool NT>
+__device__ __forceinline__ void rosenbrock_lanes(const DevProblem& pb, double (&y)[M::S], const double (&p)[PMAX],
+                                                 double* traj, int64_t W, uint32_t off, bool active, bool part,
+                                                 Acc& a) {
+  constexpr int S = M::S;
+  if constexpr (S <= kStiffRegS) {
+    integrate_rosenbrock<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, part, a);
+  } else {
+    double yc[S], pc[PMAX];
+#pragma unroll
+    for (int s = 0; s < S; ++s) yc[s] = y[s];
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) pc[q] = p[q];
+    Acc ac = a;
+    integrate_rosenbrock_big<M, PMAX, TRAJ, NT>(pb, yc, pc, traj, W, off, active, part, ac);
+#pragma unroll
+    for (int s = 0; s < S; ++s) y[s] = yc[s];
+    a = ac;
+  }
+}
+
 }  // namespace oe

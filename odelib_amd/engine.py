@@ -24,6 +24,9 @@ from . import _native as N
 METHODS = {"rk4": N.OE_METHOD_RK4, "dopri5": N.OE_METHOD_DOPRI5, "auto": N.OE_METHOD_AUTO,
            "rosenbrock": N.OE_METHOD_ROSENBROCK}
 ODEINT_TOL = 1.49012e-8  # scipy.integrate.odeint default rtol/atol (Framework.py:656)
+# widest model for which a defaulted method 'auto' stays 'auto' (the register-resident
+# stiff path, ode_kernels.cuh kStiffRegS); wider models default to 'dopri5'
+AUTO_DEFAULT_MAX_STATES = 8
 
 
 @dataclass
@@ -47,8 +50,9 @@ class FitProblem:
     max_steps: int = 500
     custom_source: str | None = None        # user RHS body for hipRTC (model_id ignored)
     auto_fallback: bool = False             # method 'auto' was a default: use 'dopri5' where
-                                            # the stiff methods are unavailable (S > 8, C body
-                                            # without a dual-number instantiation)
+                                            # the stiff methods are unavailable (S > 32, C body
+                                            # without a dual-number instantiation) or slow
+                                            # (S > AUTO_DEFAULT_MAX_STATES)
 
     def __post_init__(self):
         self.times = np.ascontiguousarray(self.times, dtype=np.float64)
@@ -193,6 +197,12 @@ class Engine:
         c = problem.to_c()
         if problem.custom_source is not None:  # compiled once per context (cached by source)
             c.model_id = self.ctx.model_compile(problem.custom_source, problem.n_states, problem.n_params)
+        if problem.method == "auto" and problem.auto_fallback and problem.n_states > AUTO_DEFAULT_MAX_STATES:
+            # a defaulted 'auto' on a wide model: the stiff path there keeps its matrices
+            # in private memory (~20x slower per stiff walker than the register path), so
+            # the default stays the non-stiff integrator; method='auto' asks for it
+            problem.method = "dopri5"
+            c.method = METHODS["dopri5"]
         try:
             self.ctx.problem_set(c)
         except N.NativeUnsupported:

@@ -171,16 +171,55 @@ def test_transpiled_time_forced_model_with_stiff_methods():
 
 
 def test_default_method_is_auto_with_dopri5_fallback():
-    """The drop-in default is 'auto' (LSODA-like); where the stiff methods are not
-    available (here a 10-state chain) the default falls back to 'dopri5', while an
-    explicit method='auto' is refused."""
+    """The drop-in default is 'auto' (LSODA-like) up to 8 states.  Wider models default
+    to 'dopri5' (their stiff path keeps the matrices in private memory, ~20x slower per
+    stiff walker) but take an explicit method='auto'; a C body without a dual-number
+    instantiation falls back to 'dopri5' by default and refuses an explicit 'auto'."""
     from helpers import chain_problem
+    from test_gpu_rtc import ONE_I_FMA_BODY
     from odelib_amd import _native as N
     m = product_model("two_i")
     assert m.method == "auto" and m.engine().problem.method == "auto"
     d = chain_problem(10, method="auto")
     d._method_default = True  # as if no method had been given
     assert d.engine().problem.method == "dopri5"
-    e = chain_problem(10, method="auto")
+    assert chain_problem(10, method="auto").engine().problem.method == "auto"
+    d = product_model("one_i", method="auto", device_rhs=ONE_I_FMA_BODY)
+    d._method_default = True
+    assert d.engine().problem.method == "dopri5"
+    e = product_model("one_i", method="auto", device_rhs=ONE_I_FMA_BODY)
     with pytest.raises(N.NativeUnsupported):
         e.engine()
+
+
+@pytest.mark.parametrize("n", [6, 10, 20])
+@pytest.mark.parametrize("method", ["auto", "rosenbrock"])
+def test_wide_chain_stiff_methods_bitwise_vs_c_restatement(n, method):
+    """S > 8: J, the LU factors and the stage vectors in private memory, the register
+    path's arithmetic — trajectories and status bitwise equal to the C restatement on
+    a ragged two-wave ensemble with stiff lanes in both waves."""
+    from helpers import chain_problem
+    m = chain_problem(n, method=method)
+    W, stiff = (70, [3, 64, 69]) if method == "auto" else (6, [1, 4])
+    theta = _mixed_thetas("two_i", W, stiff)
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"], equal_nan=True)
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
+    assert np.array_equal(out["status"], ref["status"])
+    if method == "auto":
+        assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == sorted(stiff)
+    assert not (out["status"] & 4).any()
+
+
+def test_wide_chain_mh_auto_vs_c_restatement():
+    """MH with 'auto' on a 10-state chain, stiff proposals in both waves."""
+    from helpers import chain_problem
+    W = 70
+    m = chain_problem(10, method="auto")
+    theta = _mixed_thetas("two_i", W, [2, 66])
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    walk = np.ones(5, np.uint8)
+    dev = m.engine().mh_run(theta, y0, nits=6, burnin=2, walk_mask=walk, rng="philox", seed=5)
+    ref = rk_ref.mh_run(m.fit_problem(), theta, y0, 6, 2, walk, rng="philox", seed=5)
+    np.testing.assert_allclose(dev["samples"].cpu().numpy(), ref["samples"], rtol=1e-8)

@@ -1,5 +1,5 @@
 """Kernel time of the adaptive methods on the C2 workload (two_i, 65 536 walkers, demo
-draws) with a fraction of the walkers made stiff (tau raised), per method:
+draws; --model chain<N> for the wider chains) with a fraction of the walkers made stiff (tau raised), per method:
 
     python tools/stiff_bench.py --fracs 0 0.001 0.01 --taus 1e5 1e6
 
@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--walkers", type=int, default=65536)
+    ap.add_argument("--model", default="two_i", help="two_i | chain<N> (same five parameters)")
     ap.add_argument("--fracs", type=float, nargs="+", default=[0.0, 0.001, 0.01])
     ap.add_argument("--taus", type=float, nargs="+", default=[1e5, 1e6])
     ap.add_argument("--methods", nargs="+", default=["dopri5", "auto", "rosenbrock"])
@@ -33,7 +34,7 @@ def main():
     W = args.walkers
     engines = {}
     for method in args.methods:
-        m, y0h = bench.build_problem("two_i", method, 1000)
+        m, y0h = bench.build_problem(args.model, method, 1000)
         engines[method] = m.engine()
     y0 = torch.as_tensor(np.repeat(y0h[:, None], W, axis=1), device=dev).contiguous()
     base = bench.synthetic_walkers(W, 5)
@@ -54,7 +55,7 @@ def main():
                     if r:
                         ms.append(eng.last_kernel_ms())
                 st = out["status"].cpu().numpy()
-                print(json.dumps({"walkers": W, "stiff_frac": frac, "tau": tau, "method": method,
+                print(json.dumps({"model": args.model, "walkers": W, "stiff_frac": frac, "tau": tau, "method": method,
                                   "kernel_ms": round(float(np.median(ms)), 4),
                                   "stiff_flagged": int(((st & 8) != 0).sum()), "maxstep": int(((st & 4) != 0).sum()),
                                   "trajectory": bool(args.trajectory)}), flush=True)
