@@ -95,6 +95,8 @@ struct oe_ctx {
   size_t draws_bytes = 0;
   void* np_state = nullptr;  // numpy legacy RandomState per chain (key [W][624], pos, gauss, has)
   size_t np_state_bytes = 0;
+  int32_t* stiff_buf = nullptr;  // wide-model stiff redo: [count][list W][status W]
+  size_t stiff_cap = 0;          // walkers it holds
 };
 
 namespace {
@@ -113,6 +115,26 @@ int fail(oe_ctx* c, int code, const std::string& msg) {
     if (e_ != hipSuccess)                                                              \
       return fail(ctx, OE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
+
+// ids of the walkers an 'auto' pass marked ST_STIFF (any order: each is redone on its own)
+__global__ void k_stiff_list(const int32_t* __restrict__ status, int64_t W, int32_t* __restrict__ list,
+                             int32_t* __restrict__ count) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < W && (status[w] & ST_STIFF)) list[atomicAdd(count, 1)] = (int32_t)w;
+}
+
+int ensure_stiff_buf(oe_ctx* c, int64_t W) {
+  if ((int64_t)c->stiff_cap >= W) return OE_OK;
+  if (c->stiff_buf) {
+    OE_HIP(c, hipStreamSynchronize(c->stream));
+    OE_HIP(c, hipFree(c->stiff_buf));
+    c->stiff_buf = nullptr;
+    c->stiff_cap = 0;
+  }
+  OE_HIP(c, hipMalloc(&c->stiff_buf, sizeof(int32_t) * (size_t)(2 * W + 64)));
+  c->stiff_cap = (size_t)W;
+  return OE_OK;
+}
 
 int ensure_scratch(oe_ctx* c, size_t bytes) {
   if (c->scratch_bytes >= bytes) return OE_OK;
@@ -262,6 +284,7 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->draws) (void)hipFree(c->draws);
     if (c->np_state) (void)hipFree(c->np_state);
+    if (c->stiff_buf) (void)hipFree(c->stiff_buf);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (auto& m : c->custom)
@@ -513,7 +536,35 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     ia.xcd_remap = (flags & OE_NO_XCD_REMAP) ? 0
                    : (flags & OE_XCD_RANGES) ? (int32_t)std::max<int64_t>(1, (int64_t)grid.x / 8)
                                              : (int32_t)std::max<int64_t>(1, run_walkers / per_block);
-    OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));
+    // Models wider than the register-resident stiff path: 'auto' marks the walkers the
+    // DOPRI5 pass evicts, and k_stiff_wave redoes them one wave per walker; 'rosenbrock'
+    // is k_stiff_wave for every walker (stiff_wave.cuh).
+    const bool wave_stiff = (c->method == OE_METHOD_AUTO || c->method == OE_METHOD_ROSENBROCK) &&
+                            S > kStiffRegS && (e->rtc ? e->rtc->stiff_wave[0][0] != nullptr : e->stiff_wave[0][0] != nullptr);
+    StiffWaveArgs sa{};
+    if (wave_stiff) {
+      rc = ensure_stiff_buf(c, W);
+      if (rc) return rc;
+      sa.y0 = ia.y0; sa.theta = ia.theta; sa.traj = ia.traj; sa.chi = ia.chi; sa.ssres = ia.ssres; sa.W = W;
+      if (!ia.status) ia.status = c->stiff_buf + 64 + W;  // the marks need a status array
+      sa.status = ia.status;
+    }
+    if (!(wave_stiff && c->method == OE_METHOD_ROSENBROCK))
+      OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));
+    if (wave_stiff) {
+      const dim3 wgrid((unsigned)std::min<int64_t>(W, (int64_t)16 * c->n_cu)), wblock(64);
+      if (c->method == OE_METHOD_AUTO) {
+        int32_t* count = c->stiff_buf;
+        int32_t* list = c->stiff_buf + 64;
+        OE_HIP(c, hipMemsetAsync(count, 0, sizeof(int32_t), c->stream));
+        hipLaunchKernelGGL(k_stiff_list, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, c->stream, ia.status, W,
+                           list, count);
+        OE_HIP(c, hipGetLastError());
+        sa.list = list;
+        sa.count = count;
+      }
+      OE_HIP(c, launch_stiff_wave_entry(e, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, sa, wgrid, wblock, c->stream));
+    }
   }
   OE_HIP(c, hipGetLastError());
   if (timing) OE_HIP(c, hipEventRecord(c->ev1, c->stream));

@@ -11,6 +11,7 @@ namespace oe {
 // ---- dispatch table ---------------------------------------------------------
 using IntegrateLaunch = void (*)(const DevProblem&, const IntegrateArgs&, dim3, dim3, hipStream_t);
 using MHLaunch = void (*)(const DevProblem&, const MHArgs&, dim3, dim3, hipStream_t);
+using StiffWaveLaunch = void (*)(const DevProblem&, const StiffWaveArgs&, dim3, dim3, hipStream_t);
 
 struct Entry {
   int32_t model_id;
@@ -20,6 +21,7 @@ struct Entry {
   IntegrateLaunch integrate[4][2][2];
   IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > 8
   MHLaunch mh[4];
+  StiffWaveLaunch stiff_wave[2][2];  // [traj][nt]: S > kStiffRegS stiff redo, one wave per walker
   const RtcModule* rtc = nullptr;  // user RHS compiled at run time (launchers above unused)
 };
 
@@ -59,6 +61,21 @@ template <class M, int METHOD>
 void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_mh<M, METHOD>), g, b, 0, s, pb, ma);
 }
+template <class M, bool TRAJ, bool NT>
+void launch_stiff_wave(const DevProblem& pb, const StiffWaveArgs& sa, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_stiff_wave<M, TRAJ, NT>), g, b, 0, s, pb, sa);
+}
+inline hipError_t launch_stiff_wave_entry(const Entry* e, int traj, int nt, const DevProblem& dp,
+                                          const StiffWaveArgs& sa, dim3 g, dim3 b, hipStream_t s) {
+  if (e->rtc) {
+    DevProblem a0 = dp;
+    StiffWaveArgs a1 = sa;
+    void* args[] = {(void*)&a0, (void*)&a1};
+    return hipModuleLaunchKernel(e->rtc->stiff_wave[traj][nt], g.x, g.y, g.z, b.x, b.y, b.z, 0, s, args, nullptr);
+  }
+  e->stiff_wave[traj][nt](dp, sa, g, b, s);
+  return hipGetLastError();
+}
 
 template <class M, int METHOD>
 void fill_method(Entry& e) {
@@ -80,6 +97,12 @@ Entry make_entry(int32_t model_id) {
   if constexpr (M::S <= kStiffMaxS) {
     fill_method<M, kAuto>(e);
     fill_method<M, kRosenbrock>(e);
+  }
+  if constexpr (M::S > kStiffRegS && M::S <= kStiffMaxS) {
+    e.stiff_wave[0][0] = launch_stiff_wave<M, false, false>;
+    e.stiff_wave[0][1] = launch_stiff_wave<M, false, false>;
+    e.stiff_wave[1][0] = launch_stiff_wave<M, true, false>;
+    e.stiff_wave[1][1] = launch_stiff_wave<M, true, true>;
   }
   if constexpr (M::S <= 8) {
     e.rk4_piped[0][0] = launch_rk4_piped<M, false, 2>;

@@ -789,7 +789,10 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
 #include "stiff.cuh"
 namespace oe {
 
-template <class M, int PMAX, int METHOD, bool TRAJ, bool NT>
+// WAVE_REDO (batched integrate of models wider than kStiffRegS): 'auto' only marks the
+// walkers the DOPRI5 pass evicts (status ST_STIFF); k_stiff_wave redoes them one wave per
+// walker (stiff_wave.cuh).  The MH kernel redoes them in place (private-memory path).
+template <class M, int PMAX, int METHOD, bool TRAJ, bool NT, bool WAVE_REDO = false>
 __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, int64_t w, bool active, Acc& a) {
@@ -798,6 +801,8 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
     integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
   } else if constexpr (METHOD == kDOPRI5 || M::S > kStiffMaxS) {
     integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  } else if constexpr (METHOD == kAuto && WAVE_REDO) {
+    if (integrate_dopri5<M, PMAX, TRAJ, NT, true>(pb, y, p, traj, W, off, active, a)) a.status |= ST_STIFF;
   } else if constexpr (METHOD == kAuto) {
     // LSODA-like: DOPRI5 with the stiffness test; walkers it evicts (stiff, or over the
     // step budget) are integrated again from their initial state by the Rosenbrock
@@ -889,7 +894,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
   Acc a = acc_init();
-  integrate_walker<M, PMAX, METHOD, TRAJ, NT>(pb, y, p, ia.traj, W, w, active, a);
+  integrate_walker<M, PMAX, METHOD, TRAJ, NT, (M::S > kStiffRegS)>(pb, y, p, ia.traj, W, w, active, a);
   if (active) {
     if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
     if (ia.ssres) ia.ssres[w] = a.ssres;
@@ -1271,3 +1276,4 @@ __global__ void __launch_bounds__(256)
 }
 
 }  // namespace oe
+#include "stiff_wave.cuh"

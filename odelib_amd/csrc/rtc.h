@@ -10,6 +10,7 @@ struct RtcModule {
   hipModule_t mod = nullptr;
   hipFunction_t integrate[4][2][2] = {};  // [method][traj][nt]; the stiff methods may be null
   hipFunction_t mh[4] = {};
+  hipFunction_t stiff_wave[2][2] = {};    // [traj][nt]: S > 8 with the stiff methods
   int n_methods = 0;                      // 4: RK4, DOPRI5, auto, Rosenbrock; 2: no stiff methods
 };
 

@@ -28,6 +28,10 @@ std::string rtc_integrate_name(int method, int traj, int nt) {
   return std::string("oe::k_integrate<UserModel, ") + kMethodName[method] + ", " + kBool[traj] + ", " + kBool[nt] + ">";
 }
 std::string rtc_mh_name(int method) { return std::string("oe::k_mh<UserModel, ") + kMethodName[method] + ">"; }
+std::string rtc_stiff_wave_name(int traj, int nt) {
+  return std::string("oe::k_stiff_wave<UserModel, ") + kBool[traj] + ", " + kBool[nt] + ">";
+}
+static bool has_stiff_wave(int S, int n_methods) { return n_methods == 4 && S > kStiffRegS; }
 
 std::string rtc_source(const std::string& body, int S, int P, int n_methods) {
   std::string src;
@@ -47,6 +51,11 @@ std::string rtc_source(const std::string& body, int S, int P, int n_methods) {
         src += "template __global__ void " + rtc_integrate_name(m, tr, nt) + "(const oe::DevProblem, const oe::IntegrateArgs);\n";
     src += "template __global__ void " + rtc_mh_name(m) + "(const oe::DevProblem, const oe::MHArgs);\n";
   }
+  if (has_stiff_wave(S, n_methods))
+    for (int tr = 0; tr < 2; ++tr)
+      for (int nt = 0; nt < 2; ++nt)
+        src += "template __global__ void " + rtc_stiff_wave_name(tr, nt) +
+               "(const oe::DevProblem, const oe::StiffWaveArgs);\n";
   return src;
 }
 
@@ -87,18 +96,21 @@ static int compile_program(const std::string& src, const char* arch, std::vector
   return 0;
 }
 
-static std::vector<std::string> all_names(int n_methods) {
+static std::vector<std::string> all_names(int S, int n_methods) {
   std::vector<std::string> names;
   for (int m = 0; m < n_methods; ++m)
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_integrate_name(m, tr, nt));
   for (int m = 0; m < n_methods; ++m) names.push_back(rtc_mh_name(m));
+  if (has_stiff_wave(S, n_methods))
+    for (int tr = 0; tr < 2; ++tr)
+      for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_stiff_wave_name(tr, nt));
   return names;
 }
 
 int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule* out, std::string& err) {
   int n_methods = S <= kStiffMaxS ? 4 : 2;
-  std::vector<std::string> names = all_names(n_methods), lowered;
+  std::vector<std::string> names = all_names(S, n_methods), lowered;
   std::vector<char> code;
   std::string log;
   if (compile_program(rtc_source(body, S, P, n_methods), arch, names, lowered, code, log)) {
@@ -108,7 +120,7 @@ int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule
     }
     // a body that only compiles for double (no dual-number Jacobian): no stiff methods
     n_methods = 2;
-    names = all_names(n_methods);
+    names = all_names(S, n_methods);
     std::string log2;
     if (compile_program(rtc_source(body, S, P, n_methods), arch, names, lowered, code, log2)) {
       err = "hipRTC compilation of the user RHS failed:\n" + log2;
@@ -136,6 +148,13 @@ int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule
       err = "hipModuleGetFunction failed";
       return -1;
     }
+  if (has_stiff_wave(S, n_methods))
+    for (int tr = 0; tr < 2; ++tr)
+      for (int nt = 0; nt < 2; ++nt)
+        if (hipModuleGetFunction(&out->stiff_wave[tr][nt], mod, lowered[idx++].c_str()) != hipSuccess) {
+          err = "hipModuleGetFunction failed";
+          return -1;
+        }
   return 0;
 }
 

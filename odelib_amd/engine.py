@@ -198,9 +198,10 @@ class Engine:
         if problem.custom_source is not None:  # compiled once per context (cached by source)
             c.model_id = self.ctx.model_compile(problem.custom_source, problem.n_states, problem.n_params)
         if problem.method == "auto" and problem.auto_fallback and problem.n_states > AUTO_DEFAULT_MAX_STATES:
-            # a defaulted 'auto' on a wide model: the stiff path there keeps its matrices
-            # in private memory (~20x slower per stiff walker than the register path), so
-            # the default stays the non-stiff integrator; method='auto' asks for it
+            # a defaulted 'auto' on a wide model: the MH kernel's stiff redo there keeps
+            # its matrices in private memory (~20x slower per stiff walker than the
+            # register path; the batched integrate uses one wave per stiff walker), so the
+            # default stays the non-stiff integrator; method='auto' asks for it
             problem.method = "dopri5"
             c.method = METHODS["dopri5"]
         try:

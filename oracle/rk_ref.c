@@ -46,6 +46,8 @@ typedef struct {
   const double* obs_lin;
   int method, substeps, max_steps;
   double rtol, atol;
+  int wave_redo; /* batched integrate of S > 8: stiff walkers redone one per group
+                    (odelib_amd/csrc/stiff_wave.cuh: one wave per walker, own step size) */
 } Prob;
 
 static void rhs(const Prob* pb, const double* y, double t, const double* ps, double* dy) {
@@ -764,13 +766,18 @@ static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double*
       acc_init(&L[l].a);
       L[l].a.status = ST_STIFF;
     }
-  rodas_group(pb, L, nl, p, traj, W);
+  if (pb->wave_redo) {
+    for (int l = 0; l < nl; ++l)
+      if (L[l].part) rodas_group(pb, L + l, 1, p + l * MAXP, traj, W);
+  } else {
+    rodas_group(pb, L, nl, p, traj, W);
+  }
 }
 
 static Prob make_prob(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                       const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                       int substeps, double rtol, double atol, int max_steps) {
-  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol};
+  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol, 0};
   return pb;
 }
 
@@ -811,7 +818,12 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
     auto_group(pb, L, LANES, p, traj, W);
   } else {
     for (int l = 0; l < LANES; ++l) L[l].part = L[l].active;
-    rodas_group(pb, L, LANES, p, traj, W);
+    if (pb->wave_redo) {
+      for (int l = 0; l < LANES; ++l)
+        if (L[l].part) rodas_group(pb, L + l, 1, p + l * MAXP, traj, W);
+    } else {
+      rodas_group(pb, L, LANES, p, traj, W);
+    }
   }
   for (int l = 0; l < LANES; ++l) out_acc[l] = L[l].a;
 }
@@ -822,6 +834,7 @@ int ref_integrate(int model, int S, int P, int T, const double* times, int n_obs
                   const double* theta, double* traj, double* chi, double* ssres, int32_t* status) {
   if (S > MAXS || P > MAXP || W <= 0) return -1;
   Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
+  pb.wave_redo = S > 8; /* ode_kernels.cuh kStiffRegS */
   const int64_t ngroups = (W + LANES - 1) / LANES;
   /* groups are independent: OpenMP over groups gives the same bits as the serial loop */
 #pragma omp parallel for schedule(dynamic, 4)

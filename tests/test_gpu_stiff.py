@@ -195,9 +195,10 @@ def test_default_method_is_auto_with_dopri5_fallback():
 @pytest.mark.parametrize("n", [6, 10, 20])
 @pytest.mark.parametrize("method", ["auto", "rosenbrock"])
 def test_wide_chain_stiff_methods_bitwise_vs_c_restatement(n, method):
-    """S > 8: J, the LU factors and the stage vectors in private memory, the register
-    path's arithmetic — trajectories and status bitwise equal to the C restatement on
-    a ragged two-wave ensemble with stiff lanes in both waves."""
+    """S = 6: the register path (wave-shared step); S = 10, 20: one wave per stiff
+    walker (k_stiff_wave, the walker's own step; the C restatement redoes wide walkers one
+    per group) — trajectories and status bitwise equal to the C restatement on a ragged
+    two-wave ensemble with stiff lanes in both waves."""
     from helpers import chain_problem
     m = chain_problem(n, method=method)
     W, stiff = (70, [3, 64, 69]) if method == "auto" else (6, [1, 4])
@@ -213,7 +214,8 @@ def test_wide_chain_stiff_methods_bitwise_vs_c_restatement(n, method):
 
 
 def test_wide_chain_mh_auto_vs_c_restatement():
-    """MH with 'auto' on a 10-state chain, stiff proposals in both waves."""
+    """MH with 'auto' on a 10-state chain (in-kernel redo, matrices in private memory),
+    stiff proposals in both waves."""
     from helpers import chain_problem
     W = 70
     m = chain_problem(10, method="auto")
