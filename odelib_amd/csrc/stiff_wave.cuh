@@ -235,7 +235,6 @@ __device__ __forceinline__ void rosenbrock_walker_wave(const DevProblem& pb, dou
     if (!__builtin_isfinite(hl) || !(hl > 0.0)) hl = tend - t0;
     h = fmin(hl, tend - t0);
   }
-  const double span = tend - t0;
   const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
   const int budget = kRosBudget * pb.max_steps;
   int i = 1, nst = 0;
