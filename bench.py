@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cached-stores", action="store_true", help="plain (cached) trajectory stores")
     ap.add_argument("--kernel", default="direct", choices=["direct", "pipe2", "pipe4", "pipe8"],
                     help="RK4 trajectory kernel (A/B of the opt-in producer/consumer variants)")
+    ap.add_argument("--half-waves", action="store_true",
+                    help="32 walkers per wavefront in the headline RK4 kernel (same bits; A/B)")
     ap.add_argument("--xcd", default="runs", choices=["runs", "ranges", "off"],
                     help="walker blocks per XCD: runs of 512 walkers (default), one range, blockIdx order")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
@@ -254,7 +256,7 @@ def main():
         # back-to-back launches cost ~4 % of the C1 wall time, tools/launch_gaps.py)
         return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores,
                              sync=False, timing=timing, pipelined=PIPE_ARG[args.kernel],
-                             xcd_remap=XCD_ARG[args.xcd])
+                             xcd_remap=XCD_ARG[args.xcd], half_waves=args.half_waves)
 
     # W untimed warm-up steps, continued (in batches of 5, untimed) until at least
     # --warmup-ms of launches have run: under a kernel trace the C1 kernel runs 0.33-0.38 ms
@@ -428,7 +430,7 @@ def main():
             "config": {"workload": f"{args.model} {args.method} trajectory-mode integrate + fused chi",
                        "walkers_per_gpu": Wl, "walkers_total": Wl * n_gpus, "states": S, "times": T,
                        "method": args.method, "stores": "cached" if args.cached_stores else "nontemporal",
-                       "kernel": args.kernel, "xcd": args.xcd, "parallelism": f"walker-shard x{n_gpus}"},
+                       "kernel": args.kernel + ("-half" if args.half_waves else ""), "xcd": args.xcd, "parallelism": f"walker-shard x{n_gpus}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_s * 1e3, "kernel_ms_note": "timed-region event span / steps",
