@@ -63,6 +63,13 @@ enum : int { kRK4 = 0, kDOPRI5 = 1, kAuto = 2, kRosenbrock = 3 };
 constexpr int kStiffRegS = 8;   // up to here the stiff methods factor the S x S matrix in registers,
 constexpr int kStiffMaxS = 32;  // above it in private memory (stiff.cuh); wider models: DOPRI5 only
 constexpr int kStiffTestSteps = 3;  // auto: stiffness test from the 3rd step within one output interval
+// auto: the stiffness test runs (and a lane it flags is handed to the Rosenbrock method)
+// only while the wave's step is below (t_end - t)/kStiffSwitchSteps, i.e. while finishing
+// at the stability limit would take DOPRI5 more steps than the Rosenbrock redo costs
+// (LSODA switches on cost too).  Measured on one wave without trajectory (profiles/r02zu_stiff_onewave.log): DOPRI5
+// at the stability limit ~1.1 us per step, the register RODAS redo 3-6.5 ms, so ~4000
+// steps; the wide-model in-kernel redo (MH, matrices in private memory) is ~10-20x slower.
+constexpr double kStiffSwitchSteps = 4000.0, kStiffSwitchStepsSlow = 40000.0;
 
 // per-lane accumulators of the fused likelihood
 struct Acc {
@@ -486,7 +493,7 @@ __device__ __forceinline__ double inv_fifth_root_uniform(double x, cptr<double> 
 // AUTO: Hairer's stiffness test on every accepted step (h·|λ| estimated from the last two
 // stages, ≥ 3.25 on 15 accepted steps in a row evicts the lane, as does the step
 // budget); returns whether this (active) lane was evicted, i.e. needs the stiff method.
-template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false>
+template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false, bool SLOW_REDO = false>
 __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, uint32_t off, bool active, Acc& a) {
@@ -585,12 +592,14 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
     // that will test (the same wave-uniform gate, one step ahead of the ++nst below), so
     // the stage-6 input dies before k7 instead of living through the error norm — S more
     // doubles at the kernel's register peak (same values, same order: bit-identical)
+    constexpr double kSwitch = SLOW_REDO ? kStiffSwitchStepsSlow : kStiffSwitchSteps;
     double stden_early = 0.0;
     if constexpr (AUTO && kLean) {
-      if (nst + 1 >= kStiffTestSteps) {
+      if (nst + 1 >= kStiffTestSteps && (tend - t) > kSwitch * h) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          const double dy = yn[s] - yt[s];
+          const double r = 1.0 / fma(rtol, max_abs_raw(y[s], yn[s]), atol);
+          const double dy = (yn[s] - yt[s]) * r;
           stden_early = fma(dy, dy, stden_early);
         }
       }
@@ -617,18 +626,26 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
 
     if (err <= 1.0) {
       // stiffness: h²·Σ(k7−k6)² > 3.25²·Σ(ynew − y6)² (y6 = the stage-6 input), i.e.
-      // h·|λ| > 3.25 (Hairer & Wanner I, §II.10); exact products, no square root.  Tested
+      // h·|λ| > 3.25 (Hairer & Wanner I, §II.10); exact products, no square root.  Each
+      // component is weighted by 1/(atol + rtol·max(|y|,|ynew|)), the error control's
+      // scale: unweighted, the 1e7-sized host/virus compartments swamp a stiff mode in a
+      // small compartment (two_i with tau = 1e4 or 3e4 was never flagged and crawled at
+      // 11-28 ms per integration, where RODAS takes 6 ms).  Tested
       // only on steps that stay within one output interval for the 3rd time or more (a
       // wave-uniform gate): a stiff lane pins the shared step far below the grid spacing,
       // while a non-stiff wave spans grid points with nearly every step and never pays.
-      if (AUTO && nst >= kStiffTestSteps) {
+      // The test also runs only while the shared step is below (t_end - t)/kSwitch (the
+      // cost gate above), so a mildly stiff wave that DOPRI5 finishes cheaper than the
+      // Rosenbrock redo never pays for it.
+      if (AUTO && nst >= kStiffTestSteps && (tend - t) > kSwitch * h) {
         double stnum = 0.0, stden = stden_early;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          const double dk = k7[s] - k6[s];
+          const double r = 1.0 / fma(rtol, max_abs_raw(y[s], yn[s]), atol);
+          const double dk = (k7[s] - k6[s]) * r;
           stnum = fma(dk, dk, stnum);
           if constexpr (!kLean) {
-            const double dy = yn[s] - yt[s];
+            const double dy = (yn[s] - yt[s]) * r;
             stden = fma(dy, dy, stden);
           }
         }
@@ -814,7 +831,7 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
     YI yi[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) yi[s] = y[s];
-    const bool redo = integrate_dopri5<M, PMAX, TRAJ, NT, true>(pb, y, p, traj, W, off, active, a);
+    const bool redo = integrate_dopri5<M, PMAX, TRAJ, NT, true, (S > kStiffRegS)>(pb, y, p, traj, W, off, active, a);
     if (__ballot(redo) != 0ull) {  // wave-uniform
       if (redo) {
 #pragma unroll

@@ -308,12 +308,17 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     double err = grp_max(L, nl, 1);
     ++nst;
     if (err <= 1.0) {
-      if (autom && nst >= 3) { /* ode_kernels.cuh kStiffTestSteps */
+      /* cost gate (ode_kernels.cuh kStiffSwitchSteps / kStiffSwitchStepsSlow): tested only
+         while the shared step is below (tend - t)/N */
+      const double nsw = (S <= 8 || pb->wave_redo) ? 4000.0 : 40000.0;
+      if (autom && nst >= 3 && (tend - t) > nsw * h) { /* ode_kernels.cuh kStiffTestSteps */
         for (int l = 0; l < nl; ++l) {
           Lane* q = &L[l];
+          /* components weighted by 1/(atol + rtol·max(|y|,|ynew|)), the error scale */
           double stnum = 0.0, stden = 0.0;
           for (int s = 0; s < S; ++s) {
-            double dk = q->k7[s] - q->k6[s], dy = q->yn[s] - q->yt[s];
+            double r = 1.0 / fma(rtol, fmax(fabs(q->y[s]), fabs(q->yn[s])), atol);
+            double dk = (q->k7[s] - q->k6[s]) * r, dy = (q->yn[s] - q->yt[s]) * r;
             stnum = fma(dk, dk, stnum);
             stden = fma(dy, dy, stden);
           }

@@ -70,6 +70,23 @@ def test_stiff_methods_bitwise_vs_c_restatement(method, W, stiff):
     assert not (out["status"] & 4).any()
 
 
+def test_auto_moderately_stiff_walkers_bitwise_vs_c_restatement():
+    """The weighted, cost-gated stiffness test (tau = 1e3 .. 3e4 lanes in demo waves):
+    the same walkers flagged as the C restatement, trajectories bitwise."""
+    m = product_model("two_i", method="auto")
+    W = 130
+    theta = walker_thetas("two_i", W).T.copy()
+    lanes = {5: 1e3, 40: 3e3, 64: 1e4, 100: 3e4, 129: 1e4}
+    for w, tau in lanes.items():
+        theta[4, w] = tau
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"], equal_nan=True)
+    assert np.array_equal(out["status"], ref["status"])
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
+    assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == [64, 100, 129]
+
+
 @pytest.mark.parametrize("name", ["zero_i", "one_i"])
 def test_rosenbrock_other_models_bitwise(name):
     m = product_model(name, method="rosenbrock")

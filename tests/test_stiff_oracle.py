@@ -151,6 +151,24 @@ def test_stiff_methods_match_tight_implicit_solution(method):
         assert [bool(s & 8) for s in st] == [k != "nonstiff" for k in sets]
 
 
+def test_auto_switch_is_scale_invariant_and_cost_aware():
+    """The stiffness test weighs each component by the error control's scale, so a stiff
+    mode in a small compartment is seen next to the 1e7-sized host/virus states
+    (unweighted, tau = 1e4 and 3e4 were never flagged and DOPRI5 crawled 10-30x the normal
+    work); a flagged walker is handed over only while DOPRI5 would need more than ~4000
+    more steps (tau = 1e3, 3e3 stay with DOPRI5, which is cheaper there).  Every walker
+    within the 1e-6 bar of tight Radau."""
+    taus = [1e3, 3e3, 1e4, 3e4]
+    fp, theta, y0 = _problem("auto", ["nonstiff"] * len(taus))
+    theta[4, :] = taus
+    out = rk_ref.integrate(fp, y0, theta)
+    assert [bool(s & 8) for s in out["status"]] == [False, False, True, True]
+    assert not (out["status"] & 4).any()
+    for w in range(len(taus)):
+        ref = _radau(fp, y0[:, w], theta[:, w])
+        np.testing.assert_allclose(out["traj"][:, :, w], ref, rtol=1e-6, atol=1e-6, err_msg=str(taus[w]))
+
+
 def test_auto_equals_dopri5_bitwise_without_stiff_walkers():
     """The stiffness test changes no arithmetic: with no walker evicted, 'auto' is DOPRI5."""
     m = product_model("two_i")
