@@ -1,16 +1,31 @@
 """bench.py — walker-timesteps/s of the batched ODE integrate + fused likelihood on MI355X.
 
-Contract (see task README): ``python bench.py --gpus N --steps K --warmup W``; N>1 is
-launched by torchrun, one rank per GPU.  One *step* = one batched integrate of the
-rank's walkers in trajectory mode (writes traj[T][S][W] fp64, the odeint [T,S] output
-of ODElib/Framework.py:656, plus the fused chi / R² residual of :685-706).
+Contract (see task README): ``python bench.py --gpus N --steps K --warmup W``.  N > 1 runs
+one rank per GPU under torchrun: when ``--gpus N > 1`` is given without ``WORLD_SIZE`` in
+the environment, this process starts ``python -m torch.distributed.run --nproc-per-node N
+bench.py ...`` as a child (before anything touches the GPU) and exits with its code; a
+``WORLD_SIZE`` different from N is refused.  The reported throughput is always the
+walkers the ranks actually ran ÷ the max-over-ranks wall time.
+
+One *step* = one batched integrate of the rank's walkers in trajectory mode (writes
+traj[T][S][W] fp64, the odeint [T,S] output of ODElib/Framework.py:656, plus the fused
+chi / R² residual of :685-706).
 
 Workload (BASELINE.json configs[1]): 4-state SEIV ``two_i``, 65 536
 walkers per GPU, fixed-step RK4, t = linspace(0, 3, 1000), y0 = demo data
 (S 5 236 900, V 10 981 000), θ_w = θ*·exp(0.05 z_w) with numpy RandomState(0),
 observations = demo data (H = S+I1+I2, V).  Walkers shard across ranks by contiguous
-global id with no data-path collective ("scaling": "weak"); an MCMC leg
-(device Metropolis–Hastings) ends with one RCCL all-gather of the posterior block.
+global id with no data-path collective ("scaling": "weak").
+
+Legs after the headline (all in the same JSON line):
+* ``mcmc``  — device Metropolis–Hastings (RK4, Philox) over the rank's walkers; its FP64
+  roofline counts the kernel's fp64 operations with rocprofv3 PMC
+  (SQ_INSTS_VALU_{FMA,ADD,MUL}_F64) in a child pass of the same MH call.
+* ``other_configs.C4`` — BASELINE.json configs[4]: 1 048 576 walkers sharded over the
+  N ranks (131 072 per GPU at N = 8): trajectory integrate, MH (nits = 100) and the ONE
+  posterior all-gather (RCCL over xGMI; Framework.py:1037's pd.concat), each timed
+  between barriers, max over ranks.
+* ``other_configs.C2/C3`` (N = 1 only) — the other single-GPU configs, kernel time.
 
 Timing: W untimed warm-up steps, extended (untimed) to at least --warmup-ms (60 ms) of
 launches so the chip's clocks have settled (``warmup_launches`` in the line), then exactly
@@ -19,13 +34,15 @@ K back-to-back steps between a barrier + synchronize on both sides; max over ran
 Roofline: HBM, algorithmic bytes per walker-timestep = 8·S (trajectory store),
 kernel time from HIP events recorded on the stream the kernel is launched on.
 cpu_baseline: the oracle's scipy-odeint restatement of Framework.py:656-697
-(oracle/cpu_ref.py) on the host cores, bounded sample, rank 0 at N=1 only.
+(oracle/cpu_ref.py) on the host cores available to this process, bounded sample,
+rank 0 at N=1 only.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -35,6 +52,10 @@ sys.path.insert(0, ROOT)
 THETA_STAR = [7.475e-9, 1.069e-7, 19.73, 1.934, 2.799]  # twoI posterior medians (notebook:15120-15128)
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_TFS = 78.6     # MI355X FP64 vector spec
+C4_WALKERS = 1 << 20     # BASELINE.json configs[4]: 1 048 576 walkers over 8 GPUs
+C4_NITS = 100            # posterior block [49][P+5][W/G] per rank
+MH_FP64_COUNTERS = ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                    "SQ_INSTS_VALU_TRANS_F64"]
 
 
 def parse():
@@ -58,9 +79,34 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mcmc-iters", type=int, default=21, help="MCMC leg iterations (0 = skip)")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
+    ap.add_argument("--mcmc-only", action="store_true",
+                    help="run only one MCMC-leg mh_run (the PMC child pass of the MCMC roofline)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC child passes")
     ap.add_argument("--no-extra-configs", action="store_true", help="skip the C2/C3 kernel timings")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg (1 048 576 walkers over the ranks)")
+    ap.add_argument("--c4-steps", type=int, default=10, help="C4 leg: timed trajectory integrates")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def relaunch_under_torchrun(n: int) -> int:
+    """``--gpus N > 1`` without a torchrun environment: run N ranks as a child
+    ``torch.distributed.run`` (this process has not touched the GPU) and return its exit
+    code.  Never multiply one process's throughput by N."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: --gpus {n} without WORLD_SIZE; launching {n} ranks: {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    return subprocess.run(cmd).returncode
 
 
 def workload_args(args):
@@ -70,27 +116,61 @@ def workload_args(args):
     return out
 
 
+def _pmc_dir():
+    import tempfile
+    return tempfile.mkdtemp(prefix="bench_pmc_", dir=os.path.join(ROOT, "gpurun_out")
+                            if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None)
+
+
+def _profiler_usable():
+    import shutil
+    if shutil.which("rocprofv3") is None:
+        return "rocprofv3 not found"
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        # already running under rocprofv3, whose library has initialised the GPU in this
+        # process: a child launched from here would be an exec after GPU initialisation
+        return "skipped (running under rocprofv3)"
+    return None
+
+
 def pmc_traffic(args):
     """HBM bytes per dispatch of the integrate kernel from two separate rocprofv3 PMC
     passes (FETCH_SIZE, WRITE_SIZE) of this same workload, run as child processes
     before this process touches the GPU.  gfx950 correction: FETCH_SIZE x2
     (MI355X_MICROARCH.md §HBM).  Returns (bytes or None, note)."""
-    import shutil
-    import tempfile
-    if shutil.which("rocprofv3") is None:
-        return None, "rocprofv3 not found"
-    if any(k.startswith("ROCPROF") for k in os.environ):
-        # already running under rocprofv3, whose library has initialised the GPU in this
-        # process: a child launched from here would be an exec after GPU initialisation
-        return None, "skipped (running under rocprofv3)"
+    why = _profiler_usable()
+    if why:
+        return None, why
     try:
         from tools.profile import pmc_pass
-        out = tempfile.mkdtemp(prefix="bench_pmc_", dir=os.path.join(ROOT, "gpurun_out")
-                               if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None)
+        out = _pmc_dir()
         wl = workload_args(args) + ["--no-pmc"]
-        f = pmc_pass(out, "FETCH_SIZE", wl + ["--steps", "3", "--warmup", "1"], "k_integrate", 240)
-        w = pmc_pass(out, "WRITE_SIZE", wl + ["--steps", "3", "--warmup", "1"], "k_integrate", 240)
+        f = pmc_pass(out, "FETCH_SIZE", wl, "k_integrate", 240)
+        w = pmc_pass(out, "WRITE_SIZE", wl, "k_integrate", 240)
         return f["mean"] * 1024 * 2 + w["mean"] * 1024, f"rocprofv3 PMC FETCH_SIZE(x2)+WRITE_SIZE, {f['dispatches']} dispatches"
+    except BaseException as e:  # never let profiling break the bench line
+        return None, f"PMC pass failed: {e!r}"[:200]
+
+
+def pmc_mh_flops(args):
+    """fp64 operations of ONE MCMC-leg mh_run (the same call the line times), from one
+    rocprofv3 PMC pass over a child ``bench.py --mcmc-only``: SQ_INSTS_VALU_*_F64 count
+    wave-instructions, so flops = 64 lanes x (2·FMA + ADD + MUL) summed over the k_mh
+    dispatches (rocprofv3's TOTAL_64_OPS without the int64 term; every lane of a wave is
+    a walker at these walker counts).  Transcendental helper instructions (TRANS_F64:
+    rcp/rsq/sqrt approximations inside log/exp) are reported, not counted as flops."""
+    why = _profiler_usable()
+    if why:
+        return None, why
+    try:
+        from tools.profile import pmc_counts
+        base = ["--mcmc-only", "--no-cpu-baseline", "--no-extra-configs", "--no-c4", "--no-pmc",
+                "--mcmc-iters", str(args.mcmc_iters)]
+        r = pmc_counts(_pmc_dir(), MH_FP64_COUNTERS, workload_args(args), "k_mh", 240, base=base, tag="mh_fp64")
+        c = {k: v["sum"] for k, v in r.items()}
+        flops = 64.0 * (2.0 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"])
+        return {"flops": flops, "counters_sum": c, "k_mh_dispatches": r["SQ_INSTS_VALU_FMA_F64"]["dispatches"]}, \
+            "rocprofv3 PMC SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64, one pass, child bench.py --mcmc-only"
     except BaseException as e:  # never let profiling break the bench line
         return None, f"PMC pass failed: {e!r}"[:200]
 
@@ -99,7 +179,7 @@ PIPE_ARG = {"direct": False, "pipe2": 2, "pipe4": 4, "pipe8": 8}
 XCD_ARG = {"runs": True, "ranges": "ranges", "off": False}
 
 
-def build_problem(model: str, method: str, T: int):
+def build_problem(model: str, method: str, T: int, rk4_substeps: int = 1):
     """FitProblem for the bench workload (host-side set-up only)."""
     import numpy as np
     import pandas as pd
@@ -117,7 +197,7 @@ def build_problem(model: str, method: str, T: int):
     pn = ["mu", "phi", "beta", "lam", "tau"]
     m = ModelFramework(ODE=ode, parameter_names=pn, state_names=snames, dataframe=df,
                        state_summations={"H": snames[:-1]}, t_steps=T, S=5236900, method=method,
-                       device_model="two_i" if model == "two_i" else "chain",
+                       rk4_substeps=rk4_substeps, device_model="two_i" if model == "two_i" else "chain",
                        **{p: parameter(init_value=v) for p, v in zip(pn, THETA_STAR)})
     return m, np.asarray(m.get_inits(), float)
 
@@ -129,6 +209,34 @@ def synthetic_walkers(n_total: int, P: int):
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
+def host_cores():
+    """CPU cores this process may use: its affinity set, bounded by a cgroup v2 CPU quota
+    if one is set (``/sys/fs/cgroup/cpu.max``).  Returns (cores, detail)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, {"sched_getaffinity": aff, "cgroup_cpu_max_cores": quota, "os_cpu_count": os.cpu_count(),
+                   "OMP_NUM_THREADS_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def _cpu_worker(args):
     model, times, wall_budget, theta_cols, y0, tidx, mask, O, Ssig = args
     import numpy as np
@@ -149,10 +257,11 @@ def _cpu_worker(args):
 
 
 def cpu_baseline(model, fp, y0, budget_s, P):
-    """Oracle (scipy odeint, the reference's integrator) on the host cores; fork-based
-    pool started before this process initialises the GPU."""
+    """Oracle (scipy odeint, the reference's integrator) on every host core available to
+    this process (``Pool(processes=cores)`` as Framework.py:779); fork-based pool started
+    before this process initialises the GPU."""
     import multiprocessing as mp
-    cores = min(16, os.cpu_count() or 1)
+    cores, detail = host_cores()
     theta = synthetic_walkers(cores * 16384, P)
     jobs = [(model, fp.times, budget_s, [theta[:, w] for w in range(c, theta.shape[1], cores)], y0,
              fp.obs_tidx, fp.obs_mask, fp.obs_log, fp.obs_logsigma) for c in range(cores)]
@@ -163,19 +272,11 @@ def cpu_baseline(model, fp, y0, budget_s, P):
     wall = time.perf_counter() - t0
     walkers = sum(r[0] for r in res)
     T = len(fp.times)
-    cpu_model = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
     return {"value": walkers * (T - 1) / wall, "unit": "walker-timesteps/s", "cores": cores, "kind": "port",
+            "cores_detail": detail,
             "sample": f"{walkers} walkers x {T - 1} intervals: scipy odeint (LSODA, default tol) + summation + "
                       f"masked chi (oracle/cpu_ref.py), multiprocessing.Pool({cores}) for {wall:.1f} s wall; "
-                      f"CPU: {cpu_model}"}
+                      f"CPU: {_cpu_model()}"}
 
 
 def cpu_rk4_c(fp, y0, W, cores):
@@ -201,61 +302,313 @@ def cpu_rk4_c(fp, y0, W, cores):
                       f"(oracle/rk_ref.c, gcc -O2, OpenMP {cores} threads), best of 2: {best:.2f} s"}
 
 
+# ------------------------------------------------------------------ GPU legs
+class Ranks:
+    """This rank's device and the collectives the timing needs (barrier, max)."""
+
+    def __init__(self, world, rank, local_rank):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world, self.rank = world, rank
+        # one process per GPU; ODELIB_BENCH_BACKEND=gloo lets several ranks share one GPU to
+        # rehearse the multi-rank path (the driver's N>1 runs use nccl = RCCL over xGMI)
+        self.backend = os.environ.get("ODELIB_BENCH_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
+        self.dev_index = local_rank % max(ndev, 1)
+        torch.cuda.set_device(self.dev_index)
+        self.dev = torch.device("cuda", self.dev_index)
+        if world > 1:
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(self.backend)
+        self.red_dev = self.dev if self.backend == "nccl" else torch.device("cpu")
+
+    def fence(self):
+        """barrier + synchronize (both sides of every timed region)."""
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize(self.dev)
+
+    def max(self, *vals):
+        if self.world == 1:
+            return vals if len(vals) > 1 else vals[0]
+        t = self.torch.tensor(list(vals), dtype=self.torch.float64, device=self.red_dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        out = tuple(float(x) for x in t.cpu())
+        return out if len(out) > 1 else out[0]
+
+    def engine(self, model, method, T, rk4_substeps=1):
+        m, y0h = build_problem(model, method, T, rk4_substeps)
+        m.device = self.dev_index  # this rank's GPU (the model's default device is 0)
+        eng = m.engine()
+        assert eng.device == self.dev_index
+        return eng, y0h
+
+
+def warm(fn, min_s=0.06, first=1):
+    """Untimed launches until at least ``min_s`` of wall time has passed (clocks settle)."""
+    import torch
+    n, t0 = 0, time.perf_counter()
+    while n < first or time.perf_counter() - t0 < min_s:
+        fn()
+        n += 1
+        if n % 5 == 0 or n == first:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    return n
+
+
+def mcmc_leg(args, R, eng, theta, y0, Wl, T, S, P, only=False):
+    """Device Metropolis–Hastings (RK4, Philox) over the rank's walkers."""
+    import numpy as np
+    nits = args.mcmc_iters
+    burn = nits // 2
+    walk = np.ones(P, np.uint8)
+    off = R.rank * Wl
+    if only:  # PMC child pass: exactly the dispatches of one mh_run
+        eng.mh_run(theta, y0, nits=nits, burnin=burn, walk_mask=walk, rng="philox", seed=1234, walker_offset=off)
+        return None
+    eng.mh_run(theta, y0, nits=2, burnin=0, walk_mask=walk, rng="philox", seed=1)  # load the kernel
+    R.fence()
+    tm0 = time.perf_counter()
+    r = eng.mh_run(theta, y0, nits=nits, burnin=burn, walk_mask=walk, rng="philox", seed=1234, walker_offset=off)
+    R.fence()
+    t_mh = R.max(time.perf_counter() - tm0)
+    mh_kernel_ms = eng.last_kernel_ms()
+    # the same chains with the reference's numpy legacy streams generated on the device
+    # (seed = global chain index, one lognorm prior draw per parameter)
+    seeds = np.arange(off, off + Wl)
+    eng.mh_run(theta, y0, nits=nits, burnin=burn, walk_mask=walk, rng="numpy", numpy_seeds=seeds, prior_draws=P)
+    np_kernel_ms = eng.last_kernel_ms()
+    # Fitting-report statistics of the pooled posterior (rawstats, Framework.py:11-17)
+    # from two all-reduces of per-parameter sufficient statistics
+    from odelib_amd.distributed import pooled_rawstats
+    pooled_rawstats(r["samples"], P)  # untimed: first use loads torch's reduction kernels
+    R.fence()
+    tr0 = time.perf_counter()
+    med, _ = pooled_rawstats(r["samples"], P)
+    t_rs = time.perf_counter() - tr0
+    mh_wts = R.world * Wl * (T - 1) * nits  # a-priori integrate + nits-1 proposals
+    out = {"workload": f"two_i RK4 Metropolis-Hastings, {Wl} chains per GPU, Philox draws, chi only",
+           "iterations": nits, "walker_timesteps_per_s": mh_wts / t_mh, "wall_s": t_mh,
+           "kernel_ms": mh_kernel_ms, "kernel_ms_note": "events around the whole mh_run (k_mh + k_philox_draws)",
+           "kernel_ms_numpy_rng": np_kernel_ms, "rawstats_allreduce_s": t_rs,
+           "posterior_median": [float(x) for x in med], "rng": "philox"}
+    return out
+
+
+def mcmc_roofline(mh, flops_pmc, note, Wl, T, nits):
+    """FP64-VALU roofline of the MCMC leg: PMC-counted fp64 flops of the k_mh dispatches
+    ÷ the mh_run's kernel span."""
+    if flops_pmc is None:
+        return {"bound": "fp64-valu", "achieved": None, "peak": FP64_VALU_TFS, "unit": "TFLOP/s", "frac": None,
+                "note": note}
+    f = flops_pmc["flops"]
+    ach = f / (mh["kernel_ms"] / 1e3) / 1e12
+    return {"bound": "fp64-valu", "achieved": ach, "peak": FP64_VALU_TFS, "unit": "TFLOP/s",
+            "frac": ach / FP64_VALU_TFS, "flops_per_mh_run": f,
+            "flops_per_walker_timestep": f / (Wl * (T - 1) * nits),
+            "k_mh_dispatches": flops_pmc["k_mh_dispatches"], "counters_sum": flops_pmc["counters_sum"],
+            "source": note, "time": "kernel_ms (span includes the small k_philox_draws launches)"}
+
+
+def c4_leg(args, R, T, P):
+    """BASELINE.json configs[4]: 1 048 576 two_i walkers sharded over the ranks (contiguous
+    global ids), RK4 trajectory integrate + MH (Philox keyed by global id) + the ONE
+    posterior all-gather.  Every phase is timed between barriers, max over ranks."""
+    import numpy as np
+    import torch
+    from odelib_amd.distributed import allgather_walkers, shard
+    off, cnt = shard(C4_WALKERS, R.rank, R.world)
+    eng, y0h = R.engine("two_i", "rk4", T)
+    theta_all = synthetic_walkers(C4_WALKERS, P)
+    theta = torch.as_tensor(np.ascontiguousarray(theta_all[:, off:off + cnt]), device=R.dev)
+    y0 = torch.as_tensor(np.repeat(y0h[:, None], cnt, axis=1), device=R.dev).contiguous()
+    S = len(y0h)
+    res = {"workload": f"two_i RK4, {C4_WALKERS} walkers sharded over {R.world} GPU(s) "
+                       f"({cnt} on rank {R.rank}): trajectory integrate, MH nits={C4_NITS}, posterior all-gather",
+           "walkers_total": C4_WALKERS, "walkers_per_gpu": cnt, "n_gpus": R.world}
+    # (1) trajectory-mode integrate, K back-to-back launches
+    traj = eng.empty_traj(cnt)
+
+    def step():
+        return eng.integrate(y0, theta, trajectory=True, traj_out=traj, sync=False, timing=False)
+    warm(step)
+    K = args.c4_steps
+    R.fence()
+    stream = torch.cuda.current_stream(R.dev)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for _ in range(K):
+        out = step()
+    ev[1].record(stream)
+    R.fence()
+    wall, kms = R.max(time.perf_counter() - t0, ev[0].elapsed_time(ev[1]) / K)
+    res["integrate"] = {"steps": K, "ms_per_step": wall / K * 1e3, "kernel_ms_max_rank": kms,
+                        "walker_timesteps_per_s": C4_WALKERS * (T - 1) * K / wall,
+                        "hbm_frac_per_gpu": cnt * (T - 1) * 8 * S / (kms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                        "chi_finite": bool(torch.isfinite(out["chi"]).all().item())}
+    del traj, out
+    torch.cuda.empty_cache()
+    # (2) MH over the shard, Philox keyed by the global walker id
+    walk = np.ones(P, np.uint8)
+    burn = C4_NITS // 2
+    eng.mh_run(theta[:, :256], y0[:, :256], nits=2, burnin=0, walk_mask=walk, rng="philox", seed=1)
+    R.fence()
+    t0 = time.perf_counter()
+    r = eng.mh_run(theta, y0, nits=C4_NITS, burnin=burn, walk_mask=walk, rng="philox", seed=4242, walker_offset=off)
+    R.fence()
+    t_mh = R.max(time.perf_counter() - t0)
+    res["mh"] = {"iterations": C4_NITS, "burnin": burn, "wall_s": t_mh,
+                 "walker_timesteps_per_s": C4_WALKERS * (T - 1) * C4_NITS / t_mh,
+                 "kernel_ms_rank0": eng.last_kernel_ms()}
+    # (3) the ONE posterior all-gather (Framework.py:1037 pd.concat analogue)
+    blk = r["samples"]
+    res["posterior_block_bytes_per_rank"] = blk.numel() * 8
+    if R.world > 1:
+        src = blk.contiguous() if R.backend == "nccl" else blk.cpu()
+        allgather_walkers(src[:1], C4_WALKERS)  # untimed: communicator / channel set-up
+        R.fence()
+        t0 = time.perf_counter()
+        pooled = allgather_walkers(src, C4_WALKERS)
+        R.fence()
+        t_ag = R.max(time.perf_counter() - t0)
+        assert pooled.shape[-1] == C4_WALKERS
+        gathered = pooled.numel() * 8
+        res["allgather"] = {"backend": R.backend, "bytes_gathered": gathered, "s": t_ag,
+                            "algbw_GBps": gathered / t_ag / 1e9,
+                            "busbw_GBps": gathered * (R.world - 1) / R.world / t_ag / 1e9}
+        del pooled
+    else:
+        res["allgather"] = None  # one GPU: nothing to pool
+    del r, blk
+    torch.cuda.empty_cache()
+    return res
+
+
+def extra_configs(args, R, T, P):
+    """The other single-GPU configs of BASELINE.json (C2, C3), kernel time only."""
+    import numpy as np
+    import torch
+    extra = {}
+    # C2-stiffmix: the C2 draws with 0.1 % of the walkers made stiff (tau = 1e5, the I1
+    # compartment relaxing 4e4x faster): 'dopri5' keeps them in the shared step, so their
+    # waves crawl at the stability limit; 'auto' (the drop-in default, LSODA-like) hands
+    # them to the Rosenbrock method (DESIGN.md §3.6).
+    # C3 at rk4_substeps=1 is within rtol 1e-6 / atol 1e-4 of tight odeint (SURVEY §8c's
+    # 20-state RK4 tolerance; tests/test_gpu_parity.py::test_c3_rk4_bench_accuracy);
+    # rk4_substeps=3 is within rtol = atol = 1e-6 (2 is not: 1.09 of that budget).
+    cfgs = (("C2", "two_i", "dopri5", 65536, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"),
+            ("C2-auto", "two_i", "auto", 65536, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"),
+            ("C2-stiffmix-dopri5", "two_i", "dopri5", 65536, 1e-3, 1, "rtol=atol=1.49012e-8"),
+            ("C2-stiffmix-auto", "two_i", "auto", 65536, 1e-3, 1, "rtol=atol=1.49012e-8"),
+            ("C3", "chain20", "rk4", 262144, 0.0, 1, "vs tight odeint: rtol 1e-6, atol 1e-4 (test-pinned)"),
+            ("C3-rk4x3", "chain20", "rk4", 262144, 0.0, 3, "vs tight odeint: rtol 1e-6, atol 1e-6 (test-pinned)"),
+            ("C3-dopri5", "chain20", "dopri5", 262144, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"))
+    for name, model, method, W, stiff, subs, tol in cfgs:
+        ex, y0x = R.engine(model, method, T, subs)
+        Sx = len(y0x)
+        thh = synthetic_walkers(W, P)
+        n_stiff = int(round(stiff * W))
+        if n_stiff:
+            thh[4, np.random.RandomState(7).choice(W, n_stiff, replace=False)] = 1e5
+        thx = torch.as_tensor(thh, device=R.dev).contiguous()
+        y0t = torch.as_tensor(np.repeat(y0x[:, None], W, axis=1), device=R.dev).contiguous()
+        trx = ex.empty_traj(W)
+        # as the headline: at least 60 ms of untimed launches first, so a compute-bound
+        # kernel (DOPRI5) is timed at the clock it sustains (C2: 0.57 ms per launch over the
+        # first 10 back-to-back launches, 0.49 over 50), then K back-to-back launches
+        # without event markers, timed by two events on the stream
+        K = 20 if not n_stiff else 3
+        warm(lambda: ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False,
+                                  xcd_remap=XCD_ARG[args.xcd]))
+        sx = torch.cuda.current_stream(R.dev)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record(sx)
+        for _ in range(K):
+            outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False,
+                                xcd_remap=XCD_ARG[args.xcd])
+        ev[1].record(sx)
+        torch.cuda.synchronize(R.dev)
+        kms = ev[0].elapsed_time(ev[1]) / K
+        byt = W * (T - 1) * 8 * Sx
+        extra[name] = {"workload": f"{model} {method}, {W} walkers, trajectory mode"
+                       + (f", {n_stiff} stiff walkers (tau=1e5)" if n_stiff else ""), "kernel_ms": kms,
+                       "timing": f"{K} back-to-back launches, events around them",
+                       "walker_timesteps_per_s": W * (T - 1) / (kms / 1e3),
+                       "hbm_frac": byt / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "tolerance": tol}
+        if method == "rk4":
+            extra[name]["rk4_substeps"] = subs
+        if n_stiff:
+            stx = outx["status"].cpu().numpy()
+            extra[name]["walkers_flagged_stiff"] = int(((stx & 8) != 0).sum())
+            extra[name]["walkers_maxstep"] = int(((stx & 4) != 0).sum())
+        del trx, thx, y0t, ex
+        torch.cuda.empty_cache()
+    return extra
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and env_world is None:
+        sys.exit(relaunch_under_torchrun(args.gpus))
+    world = int(env_world or 1)
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to report a mismatched run",
+              file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = world if world > 1 else args.gpus
     P = 5
 
-    # host-side problem set-up, then the CPU baseline (forks before the GPU is touched)
+    # host-side problem set-up, then the CPU baseline and the PMC child passes (all
+    # before this process touches the GPU)
     m, y0h = build_problem(args.model, args.method, args.times)
     fp_host = m.fit_problem()
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.mcmc_only:
         cpu = cpu_baseline(args.model, fp_host, y0h, args.cpu_seconds, P)
         if args.method == "rk4":
             cpu["rk4_c_openmp"] = cpu_rk4_c(fp_host, y0h, args.walkers, cpu["cores"])
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
-    if world == 1 and not args.no_pmc:
+    mh_flops, mh_flops_note = None, "skipped (--no-pmc, N>1 or no MCMC leg)"
+    if world == 1 and not args.no_pmc and not args.mcmc_only:
         traffic, traffic_note = pmc_traffic(args)
+        if args.mcmc_iters > 1 and args.model == "two_i":
+            mh_flops, mh_flops_note = pmc_mh_flops(args)
 
     import numpy as np
     import torch
-    import torch.distributed as dist
 
-    # one process per GPU; ODELIB_BENCH_BACKEND=gloo lets several ranks share one GPU to
-    # rehearse the multi-rank path (the driver's N>1 runs use nccl = RCCL over xGMI)
-    backend = os.environ.get("ODELIB_BENCH_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
-    dev_index = local_rank % max(ndev, 1)
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-    red_dev = dev if backend == "nccl" else torch.device("cpu")
-
-    m.device = dev_index  # this rank's GPU (the model's default device is 0)
-    eng = m.engine()
-    assert eng.device == dev_index
+    R = Ranks(world, rank, local_rank)
+    eng, _ = R.engine(args.model, args.method, args.times)
+    dev = R.dev
     fp = eng.problem
     S, T = fp.n_states, fp.n_times
     Wl = args.walkers
-    theta_all = synthetic_walkers(Wl * n_gpus, P)
+    theta_all = synthetic_walkers(Wl * world, P)
     theta = torch.as_tensor(np.ascontiguousarray(theta_all[:, rank * Wl:(rank + 1) * Wl]), device=dev)
     y0 = torch.as_tensor(np.repeat(y0h[:, None], Wl, axis=1), device=dev).contiguous()
+
+    if args.mcmc_only:
+        mcmc_leg(args, R, eng, theta, y0, Wl, T, S, P, only=True)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            R.dist.destroy_process_group()
+        return
+
     traj = eng.empty_traj(Wl)
 
-    def step(timing=False):
+    def step():
         # no timing-event markers between the timed launches (measured: markers between
         # back-to-back launches cost ~4 % of the C1 wall time, tools/launch_gaps.py)
         return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores,
-                             sync=False, timing=timing, pipelined=PIPE_ARG[args.kernel],
+                             sync=False, timing=False, pipelined=PIPE_ARG[args.kernel],
                              xcd_remap=XCD_ARG[args.xcd], half_waves=args.half_waves)
 
     # W untimed warm-up steps, continued (in batches of 5, untimed) until at least
@@ -270,9 +623,7 @@ def main():
             step()
             n_warm += 1
         torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    R.fence()
     stream = torch.cuda.current_stream(dev)  # the stream the engine launches on
     span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
@@ -280,15 +631,8 @@ def main():
     for k in range(args.steps):
         out = step()
     span[1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    R.fence()
+    elapsed = R.max(time.perf_counter() - t0)
     # average launch duration over the timed region: HIP events bracketing the K
     # back-to-back launches on the launch stream
     kern_avg_s = span[0].elapsed_time(span[1]) / args.steps / 1e3
@@ -301,148 +645,53 @@ def main():
         ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     kern_dispatch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    wts = n_gpus * Wl * (T - 1) * args.steps
+    wts = world * Wl * (T - 1) * args.steps  # walkers every rank actually ran
     value = wts / elapsed
     bytes_launch = Wl * (T - 1) * 8 * S + Wl * 8 * (S + P + 2)  # traj + y0/θ/chi/ssres
     achieved = bytes_launch / kern_avg_s / 1e9
     chi_ok = bool(torch.isfinite(out["chi"]).all().item())
+    del traj, out
+    torch.cuda.empty_cache()
 
-    # ---- MCMC leg: device Metropolis–Hastings (RK4), posterior all-gather over RCCL ----
     mcmc = None
     if args.mcmc_iters > 1:
-        nits = args.mcmc_iters
-        burn = nits // 2
-        walk = np.ones(P, np.uint8)
-        eng.mh_run(theta, y0, nits=2, burnin=0, walk_mask=walk, rng="philox", seed=1)  # load the kernel
-        torch.cuda.synchronize(dev)
-        tm0 = time.perf_counter()
-        r = eng.mh_run(theta, y0, nits=nits, burnin=burn, walk_mask=walk, rng="philox", seed=1234,
-                       walker_offset=rank * Wl)
-        torch.cuda.synchronize(dev)
-        t_mh = time.perf_counter() - tm0
-        mh_kernel_ms = eng.last_kernel_ms()
-        t_ag = 0.0
-        gathered_bytes = r["samples"].numel() * 8 * n_gpus
-        if world > 1:
-            from odelib_amd.distributed import allgather_walkers
-            blk = r["samples"].contiguous() if backend == "nccl" else r["samples"].cpu()
-            dist.barrier()
-            torch.cuda.synchronize(dev)
-            ta = time.perf_counter()
-            pooled = allgather_walkers(blk, Wl * n_gpus)  # Framework.py:1037 pd.concat analogue
-            torch.cuda.synchronize(dev)
-            t_ag = time.perf_counter() - ta
-            assert pooled.shape[-1] == Wl * n_gpus
-            tt = torch.tensor([t_mh, t_ag], dtype=torch.float64, device=red_dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t_mh, t_ag = float(tt[0]), float(tt[1])
-        # the same chains with the reference's numpy legacy streams generated on the device
-        # (seed = global chain index, one lognorm prior draw per parameter)
-        seeds = np.arange(rank * Wl, (rank + 1) * Wl)
-        eng.mh_run(theta, y0, nits=nits, burnin=burn, walk_mask=walk, rng="numpy", numpy_seeds=seeds,
-                   prior_draws=P)
-        np_kernel_ms = eng.last_kernel_ms()
-        # Fitting-report statistics of the pooled posterior (rawstats, Framework.py:11-17)
-        # from two all-reduces of per-parameter sufficient statistics
-        from odelib_amd.distributed import pooled_rawstats
-        pooled_rawstats(r["samples"], P)  # untimed: first use loads torch's reduction kernels
-        torch.cuda.synchronize(dev)
-        tr0 = time.perf_counter()
-        med, _ = pooled_rawstats(r["samples"], P)
-        t_rs = time.perf_counter() - tr0
-        mh_wts = n_gpus * Wl * (T - 1) * nits  # a-priori integrate + nits-1 proposals
-        flops_per_wts = 4 * 20 + 4 * 12  # 4 RHS x ~20 flop + RK update (4-state two_i)
-        mcmc = {"iterations": nits, "walker_timesteps_per_s": mh_wts / t_mh, "kernel_ms": mh_kernel_ms,
-                "fp64_tflops_est": Wl * (T - 1) * nits * flops_per_wts * (S / 4.0) / (mh_kernel_ms / 1e3) / 1e12,
-                "fp64_peak_tflops": FP64_VALU_TFS, "allgather_s": t_ag, "allgather_bytes": gathered_bytes,
-                "allgather_backend": backend if world > 1 else None, "rng": "philox",
-                "kernel_ms_numpy_rng": np_kernel_ms, "rawstats_allreduce_s": t_rs,
-                "posterior_median": [float(x) for x in med]}
+        mcmc = mcmc_leg(args, R, eng, theta, y0, Wl, T, S, P)
+        if args.model == "two_i":
+            mcmc["roofline"] = mcmc_roofline(mcmc, mh_flops, mh_flops_note, Wl, T, args.mcmc_iters)
 
-    # ---- the other single-GPU configs of BASELINE.json (C2, C3), kernel time only ----
-    extra = None
+    extra = {}
+    if not args.no_c4 and args.model == "two_i":
+        extra["C4"] = c4_leg(args, R, T, P)
     if world == 1 and not args.no_extra_configs:
-        extra = {}
-        # C4's per-GPU shard: 1 048 576 walkers over 8 GPUs = 131 072 per GPU (the N=8 run of
-        # this bench is weak-scaled at the metric's 65 536 walkers per GPU)
-        # C2-stiffmix: the C2 draws with 0.1 % of the walkers made stiff (tau = 1e5, the
-        # I1 compartment relaxing 4e4x faster): 'dopri5' keeps them in the shared step, so
-        # their waves crawl at the stability limit; 'auto' (the drop-in default, LSODA-like)
-        # hands them to the Rosenbrock method
-        for name, model, method, W, stiff in (("C2", "two_i", "dopri5", 65536, 0.0),
-                                              ("C2-auto", "two_i", "auto", 65536, 0.0),
-                                              ("C2-stiffmix-dopri5", "two_i", "dopri5", 65536, 1e-3),
-                                              ("C2-stiffmix-auto", "two_i", "auto", 65536, 1e-3),
-                                              ("C3", "chain20", "rk4", 262144, 0.0),
-                                              ("C3-dopri5", "chain20", "dopri5", 262144, 0.0),
-                                              ("C4-shard", "two_i", "rk4", 131072, 0.0)):
-            mx, y0x = build_problem(model, method, T)
-            mx.device = dev_index
-            ex = mx.engine()
-            Sx = len(y0x)
-            thh = synthetic_walkers(W, P)
-            n_stiff = int(round(stiff * W))
-            if n_stiff:
-                thh[4, np.random.RandomState(7).choice(W, n_stiff, replace=False)] = 1e5
-            thx = torch.as_tensor(thh, device=dev).contiguous()
-            y0t = torch.as_tensor(np.repeat(y0x[:, None], W, axis=1), device=dev).contiguous()
-            trx = ex.empty_traj(W)
-            # as the headline: untimed launches first — at least 60 ms of them, so a
-            # compute-bound kernel (DOPRI5) is timed at the clock it sustains (C2: 0.57 ms per
-            # launch over the first 10 back-to-back launches, 0.49 over 50) — then K
-            # back-to-back launches without event markers, timed by two events on the stream
-            K = 20 if not n_stiff else 3
-            tw = time.perf_counter()
-            while True:
-                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=True, timing=False,
-                                    xcd_remap=XCD_ARG[args.xcd])
-                if time.perf_counter() - tw > 0.06:
-                    break
-            sx = torch.cuda.current_stream(dev)
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record(sx)
-            for _ in range(K):
-                outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False,
-                                    xcd_remap=XCD_ARG[args.xcd])
-            ev[1].record(sx)
-            torch.cuda.synchronize(dev)
-            kms = ev[0].elapsed_time(ev[1]) / K
-            byt = W * (T - 1) * 8 * Sx
-            extra[name] = {"workload": f"{model} {method}, {W} walkers, trajectory mode"
-                           + (f", {n_stiff} stiff walkers (tau=1e5)" if n_stiff else ""), "kernel_ms": kms,
-                           "timing": f"{K} back-to-back launches, events around them",
-                           "walker_timesteps_per_s": W * (T - 1) / (kms / 1e3),
-                           "hbm_frac": byt / (kms / 1e3) / 1e9 / HBM_PEAK_GBS}
-            if n_stiff:
-                stx = outx["status"].cpu().numpy()
-                extra[name]["walkers_flagged_stiff"] = int(((stx & 8) != 0).sum())
-                extra[name]["walkers_maxstep"] = int(((stx & 4) != 0).sum())
-            del trx, thx, y0t, ex
-            torch.cuda.empty_cache()
+        extra.update(extra_configs(args, R, T, P))
 
     if rank == 0:
         line = {
             "metric": "walker-timesteps/sec, 4-state infection ODE, 65536 walkers, 1/2/4/8 MI355X"
             if args.model == "two_i" else f"walker-timesteps/sec, {S}-state chain ODE",
-            "value": value, "unit": "walker-timesteps/s", "n_gpus": n_gpus, "steps": args.steps,
-            "warmup": args.warmup, "warmup_launches": n_warm, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "value": value, "unit": "walker-timesteps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "warmup_launches": n_warm, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"{args.model} {args.method} trajectory-mode integrate + fused chi",
-                       "walkers_per_gpu": Wl, "walkers_total": Wl * n_gpus, "states": S, "times": T,
-                       "method": args.method, "stores": "cached" if args.cached_stores else "nontemporal",
-                       "kernel": args.kernel + ("-half" if args.half_waves else ""), "xcd": args.xcd, "parallelism": f"walker-shard x{n_gpus}"},
+                       "walkers_per_gpu": Wl, "walkers_total": Wl * world, "states": S, "times": T,
+                       "method": args.method, "rk4_substeps": 1,
+                       "tolerance": "vs tight odeint: rtol 1e-6, atol 1e-6 (test-pinned)",
+                       "stores": "cached" if args.cached_stores else "nontemporal",
+                       "kernel": args.kernel + ("-half" if args.half_waves else ""), "xcd": args.xcd,
+                       "parallelism": f"walker-shard x{world}",
+                       "launch": "torchrun, one rank per GPU" if world > 1 else "single process"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_s * 1e3, "kernel_ms_note": "timed-region event span / steps",
                          "kernel_ms_per_dispatch": kern_dispatch_ms, "bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "mcmc": mcmc,
-            "other_configs": extra,
+            "other_configs": extra or None,
             "chi_finite": chi_ok,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        R.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -288,7 +288,8 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (auto& m : c->custom)
-      if (m->rtc.mod) (void)hipModuleUnload(m->rtc.mod);
+      for (hipModule_t md : {m->rtc.mod, m->rtc.stiff_mod})
+        if (md) (void)hipModuleUnload(md);
     (void)hipStreamDestroy(c->own_stream);
   }
   delete c;
@@ -303,7 +304,7 @@ int oe_rtc_check(const char* rhs_body, int32_t n_states, int32_t n_params, const
   if (!rhs_body || n_states < 1 || n_states > 64 || n_params < 1 || n_params > 60)
     return fail(nullptr, OE_ERR_ARG, "oe_rtc_check: bad arguments");
   std::string err;
-  if (rtc_build(rhs_body, n_states, n_params, arch ? arch : "gfx950", nullptr, err))
+  if (rtc_build(rhs_body, n_states, n_params, arch ? arch : "gfx950", kRtcExplicit, nullptr, err))
     return fail(nullptr, OE_ERR_ARG, err);
   g_err.clear();
   return OE_OK;
@@ -323,7 +324,8 @@ int oe_model_compile(oe_ctx* c, const char* rhs_body, int32_t n_states, int32_t 
   OE_DEVICE_GUARD(c);
   auto m = std::make_unique<CustomModel>();
   std::string err;
-  if (rtc_build(rhs_body, n_states, n_params, c->arch.c_str(), &m->rtc, err)) return fail(c, OE_ERR_ARG, err);
+  if (rtc_build(rhs_body, n_states, n_params, c->arch.c_str(), kRtcExplicit, &m->rtc, err))
+    return fail(c, OE_ERR_ARG, err);
   m->body = rhs_body;
   m->entry.model_id = OE_MODEL_CUSTOM + (int32_t)c->custom.size();
   m->entry.S = n_states;
@@ -351,9 +353,13 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   if (!p) return fail(c, OE_ERR_ARG, "oe_problem_set: null problem");
   OE_DEVICE_GUARD(c);
   const Entry* e = nullptr;
+  CustomModel* cm = nullptr;
   if (p->model_id >= OE_MODEL_CUSTOM) {
     const size_t k = (size_t)(p->model_id - OE_MODEL_CUSTOM);
-    if (k < c->custom.size()) e = &c->custom[k]->entry;
+    if (k < c->custom.size()) {
+      cm = c->custom[k].get();
+      e = &cm->entry;
+    }
   } else {
     e = find_entry(p->model_id, p->n_states);
   }
@@ -372,11 +378,19 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   if (p->method < OE_METHOD_RK4 || p->method > OE_METHOD_ROSENBROCK)
     return fail(c, OE_ERR_ARG, "oe_problem_set: unknown method");
   if (p->method == OE_METHOD_AUTO || p->method == OE_METHOD_ROSENBROCK) {
-    const bool have = e->rtc ? (e->rtc->n_methods > p->method) : (e->integrate[p->method][0][0] != nullptr);
-    if (!have)
-      return fail(c, OE_ERR_UNSUPPORTED,
-                  "oe_problem_set: the stiff methods (auto, rosenbrock) need n_states <= 8 and a right-hand side "
-                  "that compiles for dual numbers (templated on its scalar type R)");
+    if (cm) {  // a user RHS: its stiff kernels are compiled the first time they are asked for
+      if (cm->rtc.stiff == 0) {
+        std::string err;
+        if (rtc_build(cm->body, e->S, e->P, c->arch.c_str(), kRtcStiff, &cm->rtc, err)) {
+          cm->rtc.stiff = -1;
+          cm->rtc.stiff_err = err;
+        }
+      }
+      if (cm->rtc.stiff != 1) return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: " + cm->rtc.stiff_err);
+    } else if (e->integrate[p->method][0][0] == nullptr) {
+      return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: the stiff methods (auto, rosenbrock) need n_states <= " +
+                                             std::to_string(kStiffMaxS));
+    }
   }
   if (p->method == OE_METHOD_RK4 && p->rk4_substeps < 1)
     return fail(c, OE_ERR_ARG, "oe_problem_set: rk4_substeps must be >= 1");

@@ -773,7 +773,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
       last_rej = true;
     }
     // ---- budget: evict the walkers that pin the wave's step ----
-    if (nst >= pb.max_steps || h < hmin) {
+    if (i < pb.T && (nst >= pb.max_steps || h < hmin)) {  // (not after the last grid point)
       if (!dead && el >= 0.5 * err) {
         dead = true;
         a.status |= ST_MAXSTEP;

@@ -6,18 +6,27 @@
 
 namespace oe {
 
+// The kernels of one user RHS, built in two parts on demand: the explicit methods (RK4,
+// DOPRI5) when the model is compiled, the stiff ones (auto, Rosenbrock: the body
+// instantiated with dual numbers, plus the one-wave-per-walker kernel for S > 8) the first
+// time a problem asks for them.
 struct RtcModule {
-  hipModule_t mod = nullptr;
-  hipFunction_t integrate[4][2][2] = {};  // [method][traj][nt]; the stiff methods may be null
+  hipModule_t mod = nullptr;              // RK4 + DOPRI5
+  hipModule_t stiff_mod = nullptr;        // auto + Rosenbrock (+ k_stiff_wave)
+  hipFunction_t integrate[4][2][2] = {};  // [method][traj][nt]; the stiff methods null until built
   hipFunction_t mh[4] = {};
-  hipFunction_t stiff_wave[2][2] = {};    // [traj][nt]: S > 8 with the stiff methods
-  int n_methods = 0;                      // 4: RK4, DOPRI5, auto, Rosenbrock; 2: no stiff methods
+  hipFunction_t stiff_wave[2][2] = {};    // [traj][nt]: S > kStiffRegS with the stiff methods
+  int stiff = 0;                          // 0: not built yet, 1: built, -1: unavailable (stiff_err)
+  std::string stiff_err;
 };
 
-// Compile (and, if out != null, load) the kernels for a user RHS body; 0 on success.
-// The stiff methods (auto, Rosenbrock) instantiate the body with dual numbers: when the
-// body does not compile for them (e.g. it declares `double` temporaries) or S > 8, the
-// module has RK4 and DOPRI5 only (n_methods = 2).
-int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule* out, std::string& err);
+enum RtcPart { kRtcExplicit = 0, kRtcStiff = 1 };
+
+// Compile (and, if out != null, load into *out) one part of the kernels of a user RHS
+// body; 0 on success, else -1 with the compiler log in err.  The stiff part needs
+// S <= kStiffMaxS and a body that compiles for dual numbers (templated on R, no `double`
+// temporaries).
+int rtc_build(const std::string& body, int S, int P, const char* arch, RtcPart part, RtcModule* out,
+              std::string& err);
 
 }  // namespace oe

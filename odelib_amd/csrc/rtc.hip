@@ -7,7 +7,8 @@
 // (C source, or transpiled from the Python callable by odelib_amd/transpile.py) and the
 // SAME kernel templates (ode_kernels.cuh, embedded at build time) are instantiated for
 // it with hiprtc for the device's gfx950 target, loaded as a module and launched with
-// hipModuleLaunchKernel.
+// hipModuleLaunchKernel.  The explicit methods are compiled with the model; the stiff
+// ones (dual-number Jacobian, the larger kernels) only when a problem first asks for them.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -31,9 +32,10 @@ std::string rtc_mh_name(int method) { return std::string("oe::k_mh<UserModel, ")
 std::string rtc_stiff_wave_name(int traj, int nt) {
   return std::string("oe::k_stiff_wave<UserModel, ") + kBool[traj] + ", " + kBool[nt] + ">";
 }
-static bool has_stiff_wave(int S, int n_methods) { return n_methods == 4 && S > kStiffRegS; }
+static bool has_stiff_wave(int S, RtcPart part) { return part == kRtcStiff && S > kStiffRegS; }
+static int first_method(RtcPart part) { return part == kRtcStiff ? 2 : 0; }
 
-std::string rtc_source(const std::string& body, int S, int P, int n_methods) {
+std::string rtc_source(const std::string& body, int S, int P, RtcPart part) {
   std::string src;
   src += "typedef unsigned long long uint64_t; typedef long long int64_t;\n";
   src += "typedef unsigned int uint32_t; typedef int int32_t;\n";
@@ -45,13 +47,13 @@ std::string rtc_source(const std::string& body, int S, int P, int n_methods) {
   src += "    (void)t;\n";
   src += body;
   src += "\n  }\n};\n";
-  for (int m = 0; m < n_methods; ++m) {
+  for (int m = first_method(part); m < first_method(part) + 2; ++m) {
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)
         src += "template __global__ void " + rtc_integrate_name(m, tr, nt) + "(const oe::DevProblem, const oe::IntegrateArgs);\n";
     src += "template __global__ void " + rtc_mh_name(m) + "(const oe::DevProblem, const oe::MHArgs);\n";
   }
-  if (has_stiff_wave(S, n_methods))
+  if (has_stiff_wave(S, part))
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)
         src += "template __global__ void " + rtc_stiff_wave_name(tr, nt) +
@@ -96,36 +98,34 @@ static int compile_program(const std::string& src, const char* arch, std::vector
   return 0;
 }
 
-static std::vector<std::string> all_names(int S, int n_methods) {
+static std::vector<std::string> all_names(int S, RtcPart part) {
   std::vector<std::string> names;
-  for (int m = 0; m < n_methods; ++m)
+  const int m0 = first_method(part);
+  for (int m = m0; m < m0 + 2; ++m)
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_integrate_name(m, tr, nt));
-  for (int m = 0; m < n_methods; ++m) names.push_back(rtc_mh_name(m));
-  if (has_stiff_wave(S, n_methods))
+  for (int m = m0; m < m0 + 2; ++m) names.push_back(rtc_mh_name(m));
+  if (has_stiff_wave(S, part))
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_stiff_wave_name(tr, nt));
   return names;
 }
 
-int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule* out, std::string& err) {
-  int n_methods = S <= kStiffMaxS ? 4 : 2;
-  std::vector<std::string> names = all_names(S, n_methods), lowered;
+int rtc_build(const std::string& body, int S, int P, const char* arch, RtcPart part, RtcModule* out,
+              std::string& err) {
+  if (part == kRtcStiff && S > kStiffMaxS) {
+    err = "the stiff methods (auto, rosenbrock) need n_states <= " + std::to_string(kStiffMaxS);
+    return -1;
+  }
+  std::vector<std::string> names = all_names(S, part), lowered;
   std::vector<char> code;
   std::string log;
-  if (compile_program(rtc_source(body, S, P, n_methods), arch, names, lowered, code, log)) {
-    if (n_methods == 2) {
-      err = "hipRTC compilation of the user RHS failed:\n" + log;
-      return -1;
-    }
-    // a body that only compiles for double (no dual-number Jacobian): no stiff methods
-    n_methods = 2;
-    names = all_names(S, n_methods);
-    std::string log2;
-    if (compile_program(rtc_source(body, S, P, n_methods), arch, names, lowered, code, log2)) {
-      err = "hipRTC compilation of the user RHS failed:\n" + log2;
-      return -1;
-    }
+  if (compile_program(rtc_source(body, S, P, part), arch, names, lowered, code, log)) {
+    err = part == kRtcStiff
+              ? "the stiff methods (auto, rosenbrock) need a right-hand side that compiles for dual numbers "
+                "(templated on its scalar type R); hipRTC said:\n" + log
+              : "hipRTC compilation of the user RHS failed:\n" + log;
+    return -1;
   }
   if (!out) return 0;  // compile check only
   hipModule_t mod;
@@ -133,28 +133,27 @@ int rtc_build(const std::string& body, int S, int P, const char* arch, RtcModule
     err = "hipModuleLoadData failed for the user RHS";
     return -1;
   }
-  out->mod = mod;
-  out->n_methods = n_methods;
-  int idx = 0;
-  for (int m = 0; m < n_methods; ++m)
-    for (int tr = 0; tr < 2; ++tr)
-      for (int nt = 0; nt < 2; ++nt)
-        if (hipModuleGetFunction(&out->integrate[m][tr][nt], mod, lowered[idx++].c_str()) != hipSuccess) {
-          err = "hipModuleGetFunction failed";
-          return -1;
-        }
-  for (int m = 0; m < n_methods; ++m)
-    if (hipModuleGetFunction(&out->mh[m], mod, lowered[idx++].c_str()) != hipSuccess) {
-      err = "hipModuleGetFunction failed";
-      return -1;
+  (part == kRtcStiff ? out->stiff_mod : out->mod) = mod;
+  size_t idx = 0;
+  const int m0 = first_method(part);
+  auto get = [&](hipFunction_t* f) {
+    if (hipModuleGetFunction(f, mod, lowered[idx++].c_str()) != hipSuccess) {
+      err = "hipModuleGetFunction failed for the user RHS";
+      return false;
     }
-  if (has_stiff_wave(S, n_methods))
+    return true;
+  };
+  for (int m = m0; m < m0 + 2; ++m)
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)
-        if (hipModuleGetFunction(&out->stiff_wave[tr][nt], mod, lowered[idx++].c_str()) != hipSuccess) {
-          err = "hipModuleGetFunction failed";
-          return -1;
-        }
+        if (!get(&out->integrate[m][tr][nt])) return -1;
+  for (int m = m0; m < m0 + 2; ++m)
+    if (!get(&out->mh[m])) return -1;
+  if (has_stiff_wave(S, part))
+    for (int tr = 0; tr < 2; ++tr)
+      for (int nt = 0; nt < 2; ++nt)
+        if (!get(&out->stiff_wave[tr][nt])) return -1;
+  if (part == kRtcStiff) out->stiff = 1;
   return 0;
 }
 

@@ -136,14 +136,20 @@ struct Dual {
     // constant exponent: d = b * a^(b-1) * da (finite for a <= 0 and integral b)
     return chain_(a, ::pow(a.v, b), b == 0.0 ? 0.0 : b * ::pow(a.v, b - 1.0));
   }
+  // The exponent's tangent term a^b·log(a)·db is added only where db != 0: in jac_eval the
+  // parameters are duals with zero tangents, and a base of 0 or below (a state starting at
+  // 0 raised to a parameter power, y**p) has log(a) = -inf or NaN, so the product with a
+  // zero tangent would be NaN and poison the whole Jacobian row.
   friend __host__ __device__ inline Dual pow(double a, const Dual& b) {
-    const double v = ::pow(a, b.v);
-    return chain_(b, v, v * ::log(a));
+    Dual r; r.v = ::pow(a, b.v);
+    const double dv = r.v * ::log(a);
+    OE_D_LOOP r.d[i] = b.d[i] != 0.0 ? dv * b.d[i] : 0.0;
+    return r;
   }
   friend __host__ __device__ inline Dual pow(const Dual& a, const Dual& b) {
     Dual r; r.v = ::pow(a.v, b.v);
     const double la = ::log(a.v), da = b.v * ::pow(a.v, b.v - 1.0);
-    OE_D_LOOP r.d[i] = da * a.d[i] + (r.v * la) * b.d[i];
+    OE_D_LOOP r.d[i] = b.d[i] != 0.0 ? da * a.d[i] + (r.v * la) * b.d[i] : da * a.d[i];
     return r;
   }
   friend __host__ __device__ inline Dual fmax(const Dual& a, const Dual& b) { return (b.v > a.v || a.v != a.v) ? b : a; }
@@ -473,7 +479,7 @@ __device__ __forceinline__ void integrate_rosenbrock(const DevProblem& pb, doubl
       last_rej = true;
     }
     // ---- budget: evict the walkers that pin the wave's step (as DOPRI5) ----
-    if (nst >= budget || h < hmin) {
+    if (i < pb.T && (nst >= budget || h < hmin)) {  // (not after the last grid point)
       if (!dead && el >= 0.5 * err) {
         dead = true;
         a.status |= ST_MAXSTEP;
@@ -770,7 +776,7 @@ __device__ __forceinline__ void integrate_rosenbrock_big(const DevProblem& pb, d
       h = h * fmax(facmin, safe * inv_fourth_root(err));
       last_rej = true;
     }
-    if (nst >= budget || h < hmin) {
+    if (i < pb.T && (nst >= budget || h < hmin)) {  // (not after the last grid point)
       if (!dead && el >= 0.5 * err) {
         dead = true;
         a.status |= ST_MAXSTEP;

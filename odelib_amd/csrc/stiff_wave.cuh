@@ -326,7 +326,7 @@ __device__ __forceinline__ void rosenbrock_walker_wave(const DevProblem& pb, dou
       h = h * fmax(facmin, safe * inv_fourth_root(err));
       last_rej = true;
     }
-    if (nst >= budget || h < hmin) {
+    if (i < pb.T && (nst >= budget || h < hmin)) {  // (not after the last grid point)
       // the walker pins its own step: evicted (status MAXSTEP, NaN output from here on)
       dead = true;
       a.status |= ST_MAXSTEP;

@@ -127,15 +127,22 @@ def rng_record(rng, seed, walker_offset, step_sd, walk_mask, burnin, prior_draws
     return rec
 
 
-def check_resume(resume, rec, numpy_seeds=None):
+def check_resume(resume, rec, numpy_seeds=None, allow_unverified=False):
     """Raise ValueError unless resuming ``resume`` with the draws described by ``rec``
     (``rng_record`` of the resuming call) continues the checkpointed chains exactly as
     one uninterrupted run would.  Returns the numpy seeds to use (the call's, else the
-    checkpoint's)."""
+    checkpoint's).  A checkpoint written before random-stream records existed cannot be
+    checked: it is refused unless ``allow_unverified=True`` (then resumed with a warning,
+    on the caller's word that the draws are the original ones)."""
     old = resume.get("rng_state")
     if old is None:
-        raise ValueError("the checkpoint records no random-stream state (written by an older version); "
-                         "cannot verify that resuming reproduces one uninterrupted run")
+        if not allow_unverified:
+            raise ValueError("the checkpoint records no random-stream state (written by an older version); "
+                             "cannot verify that resuming reproduces one uninterrupted run — pass "
+                             "allow_unverified=True to resume it with the draws given")
+        import warnings
+        warnings.warn("resuming a checkpoint without a random-stream record: the draws are not verified")
+        return numpy_seeds if numpy_seeds is not None else resume.get("numpy_seeds")
     for k in ("rng", "step_sd", "walk_mask", "burnin"):
         if old.get(k) != rec.get(k):
             raise ValueError(f"resume: {k}={rec.get(k)!r} differs from the checkpoint's {old.get(k)!r}")
@@ -300,7 +307,8 @@ class Engine:
 
     def mh_run(self, theta, y0, nits: int, burnin: int, walk_mask, init_param=None, rng: str = "philox",
                seed: int = 0, replay=None, step_sd: float = 0.05, walker_offset: int = 0, chunk: int = 0,
-               sync: bool = True, numpy_seeds=None, prior_draws: int = 0, resume=None):
+               sync: bool = True, numpy_seeds=None, prior_draws: int = 0, resume=None,
+               allow_unverified: bool = False):
         """Run W chains; returns dict(samples [kept][P+5][W], theta, y0, final [4][W], status).
 
         rng='replay' takes ``replay=(dz [nits-1][P][W], u [nits-1][W])`` (e.g. from
@@ -313,7 +321,8 @@ class Engine:
         one loaded by ``odelib_amd.checkpoint.load``): its theta, y0, final and status
         are the chain state after iteration ``resume['next_it'] - 1``; iterations
         next_it..nits-1 run with the same draws as one uninterrupted run, and samples
-        holds the kept rows from max(next_it, burnin+1) on."""
+        holds the kept rows from max(next_it, burnin+1) on.  ``allow_unverified`` resumes a
+        checkpoint that predates the random-stream record (see ``check_resume``)."""
         torch = self.torch
         pb = self.problem
         P, S = pb.n_params, pb.n_states
@@ -323,7 +332,7 @@ class Engine:
         rec = rng_record(rng, seed, walker_offset, step_sd, walk_mask, burnin, prior_draws, replay, nits)
         if resume is not None:
             chk = dict(rec, _replay=replay if rng == "replay" else None)
-            numpy_seeds = check_resume(resume, chk, numpy_seeds)
+            numpy_seeds = check_resume(resume, chk, numpy_seeds, allow_unverified=allow_unverified)
             it_start = int(resume["next_it"])
             theta, y0 = resume["theta"], resume["y0"]
         W = int((theta if isinstance(theta, torch.Tensor) else np.asarray(theta)).shape[1])

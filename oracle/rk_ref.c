@@ -376,7 +376,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
       h = h * fmax(0.2, 0.9 * inv_fifth_root(err));
       last_rej = 1;
     }
-    if (nst >= pb->max_steps || h < hmin) {
+    if (i < pb->T && (nst >= pb->max_steps || h < hmin)) {  /* not after the last grid point */
       for (int l = 0; l < nl; ++l)
         if (!L[l].dead && L[l].el >= 0.5 * err) {
           L[l].dead = 1;
@@ -728,7 +728,7 @@ static void rodas_group(const Prob* pb, Lane* L, int nl, const double* p, double
       h = h * fmax(0.2, 0.9 * inv_fourth_root(err));
       last_rej = 1;
     }
-    if (nst >= budget || h < hmin) {
+    if (i < pb->T && (nst >= budget || h < hmin)) {  /* not after the last grid point */
       for (int l = 0; l < nl; ++l)
         if (!L[l].dead && L[l].el >= 0.5 * err) {
           L[l].dead = 1;

@@ -187,6 +187,49 @@ def test_transpiled_time_forced_model_with_stiff_methods():
             np.testing.assert_allclose(out["traj"][:, :, w], ref, rtol=1e-6, atol=1e-6, err_msg=f"{method} {w}")
 
 
+@pytest.mark.parametrize("method", ["rosenbrock", "auto"])
+def test_transpiled_power_of_zero_state_has_finite_jacobian(method):
+    """y**p with y starting at 0 (hill_power: X(0) = 0, exponent n a parameter): the
+    dual-number Jacobian must not carry 0·log(0) = NaN from the parameter's zero tangent
+    into the row — every walker finishes within tolerance of the tight implicit solution
+    (before the fix every Rosenbrock step was rejected and the walkers were evicted)."""
+    from odelib_amd import ModelFramework, parameter
+    from test_transpile import hill_power
+    th = {"k": 2.0, "K": 1.5, "n": 2.5, "d": 0.7}
+    W = 70
+    theta = np.array(list(th.values()))[:, None] * np.exp(0.05 * np.random.RandomState(6).standard_normal((4, W)))
+    theta[3, [9, 64]] = 1e5  # stiff decay lanes (the stiff path under 'auto')
+    m = ModelFramework(ODE=hill_power, parameter_names=list(th), state_names=["X", "Y"], t_end=3.0, t_steps=300,
+                       method=method, **{k: parameter(init_value=v) for k, v in th.items()})
+    assert m.fit_problem().custom_source is not None
+    y0, out = _run(m, theta)
+    assert not (out["status"] & 5).any(), out["status"]
+    if method == "auto":
+        assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == [9, 64]
+    for w in (0, 9, 64, 69):
+        ref = _radau(hill_power, y0[:, w], m.times, theta[:, w])
+        np.testing.assert_allclose(out["traj"][:, :, w], ref, rtol=1e-6, atol=1e-6, err_msg=f"{method} {w}")
+
+
+def test_transpiled_wide_model_auto_uses_stiff_wave_kernel():
+    """A 12-state user model (loop-written chain, forced onto hipRTC) under 'auto': its
+    stiff lanes go through the hipRTC module's k_stiff_wave (one wave per stiff walker)
+    and agree with the built-in Chain<12> (same algorithm; the fused vs separate
+    multiply-subtract of the RHS moves the last bits)."""
+    from helpers import chain_problem
+    from test_transpile import chain_loop
+    a = chain_problem(12, method="auto")
+    b = chain_problem(12, method="auto", ode=chain_loop, device_model="rtc")
+    assert b.fit_problem().custom_source is not None
+    theta = _mixed_thetas("two_i", 70, [3, 64])
+    _, ra = _run(a, theta)
+    _, rb = _run(b, theta)
+    assert np.array_equal(ra["status"], rb["status"])
+    assert sorted(np.nonzero(rb["status"] & 8)[0].tolist()) == [3, 64]
+    np.testing.assert_allclose(rb["traj"], ra["traj"], rtol=1e-6, atol=1e-4)
+    np.testing.assert_allclose(rb["chi"], ra["chi"], rtol=1e-6)
+
+
 def test_default_method_is_auto_with_dopri5_fallback():
     """The drop-in default is 'auto' (LSODA-like) up to 8 states.  Wider models default
     to 'dopri5' (their stiff path keeps the matrices in private memory, ~20x slower per

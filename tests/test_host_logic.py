@@ -369,10 +369,15 @@ def test_checkpoint_records_rng_state_and_resume_checks_it(tmp_path):
     with pytest.raises(ValueError):
         check_resume(back, dict(rng_record("replay", 0, 0, 0.05, walk, 20, replay=(dz2, u), nits=40),
                                 _replay=(dz2, u)))
-    # a checkpoint without recorded state cannot be verified
-    checkpoint.save(tmp_path / "old.npz", base)
-    with pytest.raises(ValueError):
-        check_resume(checkpoint.load(tmp_path / "old.npz"), ok)
+    # a checkpoint without recorded state cannot be verified: refused, unless the caller
+    # vouches for the draws, then resumed with a warning
+    checkpoint.save(tmp_path / "old.npz", dict(base, numpy_seeds=seeds))
+    old = checkpoint.load(tmp_path / "old.npz")
+    with pytest.raises(ValueError, match="allow_unverified"):
+        check_resume(old, ok)
+    with pytest.warns(UserWarning, match="not verified"):
+        got = check_resume(old, rng_record("numpy", 0, 0, 0.05, walk, 20, prior_draws=P), allow_unverified=True)
+    assert np.array_equal(got, seeds)
 
 
 def test_resolution_never_binds_a_builtin_by_probing_alone():

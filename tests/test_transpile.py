@@ -31,6 +31,28 @@ def piecewise(y, t, ps):
     return np.array([out, abs(y[-1]) - np.maximum(x, 1.0) ** 1.5])
 
 
+def hill_power(y, t, ps):
+    """Hill-type activation with a fitted exponent: a state that starts at 0 raised to a
+    parameter power (pow(y, p) in the translation)."""
+    k, K, n, d = ps[0], ps[1], ps[2], ps[3]
+    X = y[0]
+    Y = y[1]
+    dX = k - d * X
+    dY = k * X ** n / (K ** n + X ** n) - d * Y
+    return [dX, dY]
+
+
+def test_power_of_state_translates_to_pow():
+    tr = transpile(hill_power, 2, 4)
+    assert "pow(y[0], ps[2])" in tr.c_body.replace("X", "y[0]") or "pow(" in tr.c_body
+    rs = np.random.RandomState(2)
+    for _ in range(10):
+        y = rs.uniform(0, 5, 2)
+        ps = rs.uniform(0.5, 3, 4)
+        np.testing.assert_allclose(tr.evaluate(y, 0.0, ps), hill_power(y, 0.0, ps), rtol=1e-14)
+    np.testing.assert_array_equal(tr.evaluate(np.zeros(2), 0.0, [2.0, 1.5, 2.5, 0.7]), [2.0, 0.0])
+
+
 @pytest.mark.parametrize("name", ["zero_i", "one_i", "two_i"])
 def test_demo_models_translate_exactly(name):
     f = CONFIGS[name]["ode"]

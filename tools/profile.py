@@ -55,21 +55,37 @@ def read_csv(path):
         return list(csv.DictReader(f))
 
 
-def pmc_pass(out, counter, bench_args, kernel_regex, timeout):
-    d = os.path.join(out, f"pmc_{counter.lower()}")
-    run(rocprof() + ["--pmc", counter, "--kernel-include-regex", kernel_regex, "--output-format", "csv",
-         "-d", d, "-o", "run", "--", sys.executable, "bench.py", "--no-cpu-baseline", "--mcmc-iters", "0",
-         "--no-extra-configs", "--steps", "5", "--warmup", "1", *bench_args], timeout)
+TRAJ_ONLY = ["--no-cpu-baseline", "--mcmc-iters", "0", "--no-extra-configs", "--no-c4", "--steps", "5", "--warmup", "1"]
+
+
+def pmc_counts(out, counters, bench_args, kernel_regex, timeout, base=None, tag=None):
+    """One rocprofv3 --pmc pass over ``bench.py <base> <bench_args>`` collecting
+    ``counters`` (all in ONE pass: the caller keeps them within one pass's block limits)
+    for the dispatches matching ``kernel_regex``.  Returns {counter: {dispatches, mean,
+    sum, csv}}, values summed over XCD / SE instances of each dispatch."""
+    counters = [counters] if isinstance(counters, str) else list(counters)
+    d = os.path.join(out, f"pmc_{(tag or '_'.join(counters)).lower()}")
+    run(rocprof() + ["--pmc", *counters, "--kernel-include-regex", kernel_regex, "--output-format", "csv",
+         "-d", d, "-o", "run", "--", sys.executable, "bench.py", *(TRAJ_ONLY if base is None else base),
+         *bench_args], timeout)
     path = find(os.path.join(d, "**", "*counter_collection.csv"))
     rows = read_csv(path)
-    vals = {}
-    for r in rows:
-        if r.get("Counter_Name") != counter:
-            continue
-        key = (r.get("Dispatch_Id"), r.get("Kernel_Name"))
-        vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])  # sum over XCD / instances
-    per = list(vals.values())
-    return {"dispatches": len(per), "mean": sum(per) / max(len(per), 1), "csv": os.path.relpath(path, ROOT)}
+    res = {}
+    for c in counters:
+        vals = {}
+        for r in rows:
+            if r.get("Counter_Name") != c:
+                continue
+            key = (r.get("Dispatch_Id"), r.get("Kernel_Name"))
+            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])  # sum over XCD / instances
+        per = list(vals.values())
+        res[c] = {"dispatches": len(per), "mean": sum(per) / max(len(per), 1), "sum": sum(per),
+                  "csv": os.path.relpath(path, ROOT)}
+    return res
+
+
+def pmc_pass(out, counter, bench_args, kernel_regex, timeout, base=None):
+    return pmc_counts(out, [counter], bench_args, kernel_regex, timeout, base=base)[counter]
 
 
 def main():
@@ -85,7 +101,8 @@ def main():
     # 1. kernel trace + stats (same command line as the bench run, minus the CPU leg)
     d = os.path.join(out, "trace")
     stdout = run(rocprof() + ["--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run", "--",
-                  sys.executable, "bench.py", "--no-cpu-baseline", "--no-extra-configs", "--no-pmc", *bench_args],
+                  sys.executable, "bench.py", "--no-cpu-baseline", "--no-extra-configs", "--no-c4", "--no-pmc",
+                  *bench_args],
                  args.timeout)
     bench_line = [l for l in stdout.splitlines() if l.startswith("{")]
     stats_csv = find(os.path.join(d, "**", "*kernel_stats.csv"))
