@@ -19,6 +19,9 @@
  *   oe_mh_run        <- Statistics/Samplers.py:53-174 MetropolisHastings, for W
  *                       independent chains (one per walker), i.e. the
  *                       MCMC(...) chain loop of Framework.py:1013-1030.
+ *   oe_allgather_samples <- the pd.concat of the per-process chain posteriors
+ *                       (Framework.py:1035-1038) after Pool.starmap (:779-780):
+ *                       one RCCL all-gather of the ranks' sample blocks.
  *
  * Conventions
  *   - All buffers are caller-owned.  Pointers are DEVICE pointers unless the
@@ -42,7 +45,7 @@
 extern "C" {
 #endif
 
-#define OE_ABI_VERSION 3
+#define OE_ABI_VERSION 4
 
 /* return codes */
 enum {
@@ -227,6 +230,29 @@ int oe_mh_run(oe_ctx* ctx, const oe_mh_args* args, uint32_t flags);
  * u [nits-1][W]: the replay_dz / replay_u inputs of OE_RNG_REPLAY.  Device pointers. */
 int oe_numpy_streams(oe_ctx* ctx, int64_t n_walkers, const uint32_t* seeds, int32_t nits, int32_t n_params,
                      const uint8_t* walk_mask, int32_t prior_draws, double step_sd, double* dz, double* u);
+
+/* ---- multi-GPU posterior pooling (one process per GPU, RCCL over xGMI) ----------------
+ * Ranks own contiguous global walker ids (rank r: counts[r] walkers after those of ranks
+ * < r) and run oe_mh_run with walker_offset = their first id.  Their sample blocks are
+ * pooled by ONE all-gather, the analogue of Framework.py:1037's pd.concat.
+ * The communicator is RCCL's (librccl.so opened at first use).  Rank 0 creates the id
+ * with oe_comm_unique_id and hands the 128 bytes to the other ranks by any channel (MPI,
+ * torch.distributed broadcast, a file); every rank then calls oe_comm_init with it. */
+#define OE_COMM_ID_BYTES 128
+typedef struct oe_comm oe_comm;
+int oe_comm_unique_id(uint8_t* id, int32_t id_bytes);
+int oe_comm_init(int32_t device, int32_t n_ranks, int32_t rank, const uint8_t* id, int32_t id_bytes,
+                 oe_comm** out);
+void oe_comm_destroy(oe_comm* comm);
+const char* oe_comm_last_error(const oe_comm* comm); /* NULL: the last oe_comm_init / unique_id error */
+/* Launch the collective on this hipStream_t (NULL = the null stream, the default). */
+int oe_comm_set_stream(oe_comm* comm, void* hip_stream);
+/* Every rank's block [rows][counts[rank]] (device, walker-minor, e.g. oe_mh_run's samples
+ * viewed as rows = kept*(P+5)) gathered into out [rows][sum(counts)] (device) on every
+ * rank, in global walker order.  Uneven counts are padded for the collective.  Flags:
+ * OE_ASYNC (do not synchronize the stream before returning). */
+int oe_allgather_samples(oe_comm* comm, int64_t rows, const double* block, const int64_t* counts, double* out,
+                         uint32_t flags);
 
 /* Device time (ms) of the kernel launches of the last oe_integrate / oe_mh_run,
  * from HIP events recorded on the context's stream around them (waits for them). */

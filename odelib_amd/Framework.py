@@ -4,34 +4,40 @@ MI355X batched engine.
 Same constructor, attribute names, data set-up and method signatures as the reference
 (citations inline), so user code written for ODElib runs unchanged; every integration
 and likelihood evaluation goes through ``libodelib_amd.so`` (``engine.Engine``).  The
-ODE callable is bound to a compiled device RHS by ``models.resolve``.
+ODE callable is bound to a compiled device RHS by ``models.resolve_model``.
 
 Engine options (keyword-only, new): ``method`` ('auto' default — like odeint's LSODA:
 adaptive DOPRI5 with a per-walker stiffness test, stiff walkers redone by an L-stable
 Rosenbrock method; 'dopri5' by default for models wider than 8 states or where the
 stiff methods are unavailable — or 'dopri5', 'rosenbrock', 'rk4'), ``rtol``/``atol``
-(odeint defaults), ``rk4_substeps``,
-``max_steps`` (odeint's mxstep), ``device`` (HIP device index; default: torch's current
-device when the engine is built), ``device_model``
-(force a built-in RHS, or 'rtc'), ``device_rhs`` (C++ body of the RHS for hipRTC).
-An ODE callable that matches no built-in is transpiled to C and compiled at run time.
-``MCMC`` runs every chain as one walker of a single batched launch; ``rng='replay'``
-(default) reproduces the reference's numpy draws per chain, ``rng='philox'`` draws
-on device for large ensembles.
+(odeint defaults), ``rk4_substeps``, ``max_steps`` (odeint's mxstep), ``device`` (HIP
+device index; default: torch's current device when the engine is built),
+``device_model`` (force a built-in RHS, or 'rtc'), ``device_rhs`` (C++ body of the RHS
+for hipRTC).  An ODE callable that matches no built-in is transpiled to C and compiled at
+run time.  ``MCMC`` runs every chain as one walker of a single batched launch;
+``rng='replay'`` (default) reproduces the reference's numpy draws per chain,
+``rng='philox'`` draws on device for large ensembles.
+
+Deliberate differences from the reference, all where the reference fails: a plain number
+passed for a parameter the model has not seen yet becomes a parameter (the reference
+passes it as the distribution, Framework.py:452, and crashes); ``explore_equilibriums``
+labels its state columns with the ODE state names (the reference labels them after
+summation and fails on models with state summations, Framework.py:34-35);
+``set_best_params`` skips NaN likelihoods.
 """
 from __future__ import annotations
 
 import itertools
-import random as rd
+import random
 import warnings
 
 import numpy as np
 import pandas as pd
 
+from . import datasetup
 from . import models as _models
 from .Statistics import Samplers, stats
 from .engine import ODEINT_TOL, Engine, FitProblem
-from .rng import legacy_replay_streams
 
 _ENGINE_KW = ("method", "rtol", "atol", "rk4_substeps", "max_steps", "device", "device_model", "device_rhs")
 # One token per distinct data set-up (constructor / reset_dataframe).  copy() keeps the
@@ -40,75 +46,92 @@ _DATA_TOKENS = itertools.count()
 
 
 def rawstats(pdseries):
-    """raw median and standard deviation of a posterior column (Framework.py:11-17)"""
-    log_mean = np.log(pdseries).mean()
-    median = np.exp(log_mean)
-    log_std = np.log(pdseries).std()
-    std = ((np.exp(log_std ** 2) - 1) * np.exp(2 * log_mean + log_std ** 2.0)) ** 0.5
-    return (median, std)
+    """Posterior summary of one parameter column (Framework.py:11-17): the median of a
+    log-normal fitted by moments in log space, exp(mean log x), and that log-normal's
+    standard deviation from the sample (ddof = 1) variance of log x."""
+    logs = np.log(pdseries)
+    m = logs.mean()
+    v = logs.std() ** 2
+    return np.exp(m), ((np.exp(v) - 1) * np.exp(2 * m + v)) ** 0.5
 
 
 class parameter:
-    """Parameter with a scipy prior (Framework.py:50-163)."""
+    """A fitted quantity (Framework.py:50-163): its current value ``val`` (ndarray), an
+    optional scipy prior ``dist`` with hyperparameters ``hp``, and its ``name``."""
 
     def __init__(self, stats_gen=None, hyperparameters=None, init_value=None, name=None):
         self.dist = stats_gen
         self.hp = hyperparameters
         self.name = name
-        if init_value:
-            self.val = np.array(init_value)
+        if init_value:  # as the reference: a falsy value means "draw one from the prior"
+            value = init_value
+        elif self.dist:
+            value = self.dist.rvs(**self.hp)
         else:
-            if not self.dist:
-                raise ValueError("You must specify a scipy distribution if not passing a value")
-            self.val = np.array((self.dist.rvs(**self.hp)))
+            raise ValueError("a parameter needs an init_value, or a scipy distribution (stats_gen) to draw one")
+        self.val = np.array(value)
         self._dim = self.val.shape
 
     def fit(self, data):
-        """fit the distribution to data and store its hyperparameters"""
-        shapes = self.dist.shapes.split(",") if self.dist.shapes else []
-        shapeargs = [s.strip() for s in shapes] + ["loc", "scale"]
-        vals = self.dist.fit(data)
-        if self.hp is None:
-            self.hp = {}
-        for i, arg in enumerate(shapeargs):
-            self.hp[arg] = vals[i]
+        """Fit the prior to ``data`` (scipy's ``dist.fit``) and keep the fitted
+        hyperparameters, shape parameters first, then loc and scale."""
+        names = [s.strip() for s in self.dist.shapes.split(",")] if self.dist.shapes else []
+        fitted = self.dist.fit(data)
+        self.hp = dict(self.hp or {})
+        self.hp.update(zip(names + ["loc", "scale"], fitted))
 
     def pdf(self, val=None):
-        if self.dist:
-            if val:
-                return self.dist.pdf(val, **self.hp)
-            return self.dist.pdf(self.dist.rvs(**self.hp), **self.hp)
-        return 1.0
+        """Prior density at ``val``.  With no argument the reference evaluates the density
+        at a fresh prior draw (Framework.py:103), which advances numpy's global RNG — the
+        MH sampler relies on that consumption, so it is kept."""
+        if not self.dist:
+            return 1.0
+        at = val if val else self.dist.rvs(**self.hp)
+        return self.dist.pdf(at, **self.hp)
 
     def rwalk(self, std=.05):
-        """log-normal random walk of the value (Framework.py:107-122)"""
-        stds = np.full(self._dim, std)
-        self.val = np.exp(np.log(self.val) + np.random.normal(0, stds))
+        """Log-normal random-walk proposal (Framework.py:107-122): one N(0, std) step per
+        element in log space."""
+        step = np.random.normal(0, np.full(self._dim, std))
+        self.val = np.exp(np.log(self.val) + step)
 
     def has_distribution(self):
         return bool(self.dist)
 
     def __repr__(self):
-        outstr = [str(self.val) + '  ']
+        text = str(self.val) + '  '
         if self.dist:
-            outstr.append("(distribution:{}, ".format(self.dist.name))
-            outstr.append("hyperparameters:{})".format(str(self.hp)))
-        return ' '.join(outstr)
+            text += " (distribution:{},  hyperparameters:{})".format(self.dist.name, self.hp)
+        return text
 
     __str__ = __repr__
 
     def get_figure(self, samples=1000, logspace=False):
-        s = pd.Series(self.dist.rvs(size=samples, **self.hp))
+        draws = pd.Series(self.dist.rvs(size=samples, **self.hp))
+        lo, hi = draws.min(), draws.max()
+        edges = np.logspace(np.log10(lo), np.log10(hi), 50) if logspace else np.linspace(lo, hi, 50)
+        ax = draws.hist(bins=edges)
         if logspace:
-            ax = s.hist(bins=np.logspace(np.log10(s.min()), np.log10(s.max()), 50))
             ax.figure.gca().set_xscale("log")
-        else:
-            ax = s.hist(bins=np.linspace(s.min(), s.max(), 50))
         ax.set_title(self.name)
         return ax.figure
 
     def copy(self):
         return parameter(init_value=self.val, stats_gen=self.dist, hyperparameters=self.hp, name=self.name)
+
+
+def _worker_order(n_rows: int, cores: int):
+    """Row order and index of a result the reference assembles from ``cores`` workers:
+    rows are dealt round-robin (Framework.py:787-798), workers are started last-first
+    (``worklist.pop()``) and their frames concatenated in that order, each frame indexed
+    from 0 (Framework.py:800-816)."""
+    cores = max(1, int(cores))
+    order, index = [], []
+    for w in reversed(range(cores)):
+        rows = list(range(w, n_rows, cores))
+        order += rows
+        index += range(len(rows))
+    return np.asarray(order, dtype=np.int64), np.asarray(index, dtype=np.int64)
 
 
 class ModelFramework:
@@ -139,124 +162,59 @@ class ModelFramework:
         self._engine = None
         self._data_token = next(_DATA_TOKENS)
 
-        self.parameters = {el: None for el in self._pnames}
-        self.istates = {el: 0 for el in self._snames}  # Framework.py:216
+        self.parameters = dict.fromkeys(self._pnames)
+        self.istates = dict.fromkeys(self._snames, 0)  # states default to 0 (Framework.py:216)
         self.random_seed = random_seed
+        self._set_summations(datasetup.summation_plan(self._snames, state_summations))
 
-        if state_summations:
-            (self._summations_index, self._summation_snames, self._sumkeep,
-             self._suminds) = self._get_summation_index(state_summations)
-        else:
-            self._summations_index, self._summation_snames, self._sumkeep, self._suminds = {}, tuple(), tuple(), tuple()
-
-        self._obs_logabundance = {}
-        self._obs_logsigma = {}
         self._obs_abundance = {}
         if isinstance(dataframe, pd.DataFrame):
-            self.df = self._formatdf(dataframe.copy())
-            self.times = np.linspace(0, max(self.df['time']), t_steps)  # Framework.py:234
-            self._samples = len(self.df)
-            self._pred_tindex, self._obs_logabundance, self._obs_logsigma = self._df_fitsetup()
+            self._load_data(dataframe, t_steps)
         else:
-            self.df = None
-            self._samples = None
-            self._pred_tindex = {}
+            self.df, self._samples = None, None
+            self._pred_tindex, self._obs_logabundance, self._obs_logsigma = {}, {}, {}
             self.times = np.linspace(0, t_end, t_steps)
 
-        _is, _ps = {}, {}
-        if isinstance(self.df, pd.DataFrame):  # Framework.py:246-249
-            for org, abundance in self.df[self.df['time'] == 0]['abundance'].items():
-                if org not in _is:
-                    _is[org] = abundance
-        for el in kwargs:  # Framework.py:252-256
-            if el in self._pnames:
-                _ps[el] = kwargs[el]
-            if el in self._snames:
-                _is[el] = kwargs[el]
-        self.set_parameters(**_ps)
-        self.set_inits(**_is)
-        self._pnum = 0  # Framework.py:261-263: count of non-None parameters
-        for p in self.parameters:
-            self._pnum += np.count_nonzero(self.parameters[p])
+        # initial states: observed at t = 0, then keyword arguments (Framework.py:246-256)
+        inits = datasetup.data_initial_states(self.df) if self.df is not None else {}
+        inits.update({k: v for k, v in kwargs.items() if k in self._snames})
+        self.set_parameters(**{k: v for k, v in kwargs.items() if k in self._pnames})
+        self.set_inits(**inits)
+        # AIC's parameter count: non-zero parameter elements (Framework.py:261-263)
+        self._pnum = sum(int(np.count_nonzero(p)) for p in self.parameters.values())
 
     # ------------------------------------------------------------------ data set-up
-    def reset_dataframe(self, df):
-        self.df = self._formatdf(df.copy())
-        self.times = np.linspace(0, max(self.df['time']), len(self.times))
-        self._pred_tindex, self._obs_logabundance, self._obs_logsigma = self._df_fitsetup()
+    def _set_summations(self, plan: datasetup.Summations):
+        self._summation_plan = plan
+        self._summations_index = plan.groups
+        self._summation_snames = plan.out_names
+        self._sumkeep = plan.keep
+        self._suminds = plan.labels
+
+    def _load_data(self, dataframe, t_steps):
+        self.df = self._formatdf(dataframe.copy())
+        self.times = np.linspace(0, max(self.df['time']), t_steps)  # Framework.py:234
         self._samples = len(self.df)
-        _is = {}
-        for org, abundance in self.df[self.df['time'] == 0]['abundance'].items():
-            if org not in _is:
-                _is[org] = abundance
-        self.set_inits(**_is)
+        self._pred_tindex, self._obs_logabundance, self._obs_logsigma = self._df_fitsetup()
+
+    def reset_dataframe(self, df):
+        """Fit to new data on the same grid size (Framework.py:265-279)."""
+        self._load_data(df, len(self.times))
+        self.set_inits(**datasetup.data_initial_states(self.df))
         self._data_token = next(_DATA_TOKENS)
 
     def _formatdf(self, df):
-        """normalise the two accepted dataframe layouts (Framework.py:281-307)"""
-        df = df.sort_values(by=['organism', 'time'])
-        if 'replicate' in df:
-            _df = df[['organism', 'time', 'abundance']].copy()
-            _df['log_abundance'] = np.log(_df['abundance'])
-            dfagg = _df.groupby(by=['time', 'organism']).mean()
-            dfagg['log_sigma'] = _df.groupby(by=['time', 'organism']).std()['log_abundance']
-            dfagg = dfagg.reset_index(level='time')
-            for sname in self._snames:
-                if sname in dfagg.index:
-                    self._obs_abundance[sname] = dfagg.loc[sname]['abundance'].to_numpy()
-                    self._obs_logabundance[sname] = dfagg.loc[sname]['log_abundance'].to_numpy()
-                    self._obs_logsigma[sname] = dfagg.loc[sname]['log_sigma'].to_numpy()
-            df = dfagg
-        else:
-            df = df.set_index('organism')
-            if 'abundance' in df and 'log_abundance' not in df:
-                df['log_abundance'] = np.log(df['abundance'].to_numpy())
-            if 'log_sigma' not in df:
-                df['log_sigma'] = 1
-                warnings.warn("log_sigma not found, setting log variance to 1")
-        return df
+        table, replicate_stats = datasetup.tidy_dataframe(df, self._snames)
+        for s, (ab, lab, lsig) in replicate_stats.items():
+            self._obs_abundance[s] = ab
+        return table
 
     def _df_fitsetup(self):
-        """pred_tindex = FIRST nearest grid index per observation (Framework.py:309-329)"""
-        _pred_tindex = {}
-        for pred in set(self.df.index):
-            tv = self.df.loc[pred]['time']
-            if isinstance(tv, pd.Series):
-                _pred_tindex[pred] = np.r_[[int(np.argmin(abs(a - self.times))) for a in tv]]
-            else:
-                _pred_tindex[pred] = np.r_[int(np.argmin(abs(tv - self.times)))]
-        _obs_logabundance, _obs_logsigma = {}, {}
-        for sname in self.df.index:
-            _obs_logabundance[sname] = self.df.loc[sname]['log_abundance'].to_numpy()
-            _obs_logsigma[sname] = self.df.loc[sname]['log_sigma'].to_numpy()
-        return _pred_tindex, _obs_logabundance, _obs_logsigma
+        return datasetup.observation_index(self.df, self.times)
 
     def _get_summation_index(self, summation_mapping):
-        """state summations, stored in the group's lowest index (Framework.py:332-381)"""
-        sname_i = {sname: i for i, sname in enumerate(self._snames)}
-        isum_summations, summed, i_newname = {}, set(), {}
-        for sumpop in summation_mapping:
-            summation_indices = []
-            for pop in summation_mapping[sumpop]:
-                if pop in summed:
-                    raise ValueError("{} state varaiable cannot be used in two summations".format(pop))
-                if pop not in self._snames:
-                    raise ValueError("{} state varaiable is not a valid state name".format(pop))
-                summed.add(pop)
-                summation_indices.append(sname_i[pop])
-            if len(summation_indices) < 1:
-                raise ValueError("Summation of {} has no states".format(sumpop))
-            summation_indices.sort()
-            isum = summation_indices[0]
-            i_newname[isum] = sumpop
-            isum_summations[isum] = tuple(summation_indices)
-        summation_snames, summation_keep = [], []
-        for i, sname in enumerate(self._snames):
-            if i in i_newname:
-                summation_snames.append(i_newname[i]); summation_keep.append(i)
-            elif sname not in summed:
-                summation_snames.append(sname); summation_keep.append(i)
-        return isum_summations, tuple(summation_snames), tuple(summation_keep), i_newname
+        plan = datasetup.summation_plan(self._snames, summation_mapping)
+        return plan.groups, plan.out_names, plan.keep, plan.labels
 
     # ------------------------------------------------------------------ accessors
     def get_pnames(self):
@@ -265,71 +223,54 @@ class ModelFramework:
     def get_snames(self, after_summation=True, predict_obs=False):
         if after_summation and self._summations_index:
             return list(self._summation_snames)
-        elif predict_obs:
-            return list(self._pred_tindex.keys())
+        if predict_obs:
+            return list(self._pred_tindex)
         return list(self._snames)
 
     def __repr__(self):
-        outstr = ["Current Model = {}".format(str(getattr(self._model, '__module__', '')) + '.' +
-                                              str(getattr(self._model, '__name__', self._model))),
-                  "Parameters:"]
-        for p in self.get_pnames():
-            outstr.append("\t{} = {}".format(p, self.parameters[p]))
-        outstr.append("Initial States:")
-        for s in self.get_snames(after_summation=False):
-            outstr.append("\t{} = {}".format(s, self.istates[s]))
+        fn = self._model
+        lines = [f"Current Model = {getattr(fn, '__module__', '')}.{getattr(fn, '__name__', fn)}", "Parameters:"]
+        lines += [f"\t{p} = {self.parameters[p]}" for p in self._pnames]
+        lines.append("Initial States:")
+        lines += [f"\t{s} = {self.istates[s]}" for s in self._snames]
         if self._summations_index:
-            outstr.append("Current State Summations")
-            snames = self.get_snames(after_summation=False)
-            for i in self._summations_index:
-                summed = '+'.join([snames[j] for j in self._summations_index[i]])
-                outstr.append("\t{}={}".format(str(self._suminds[i]), summed))
-        return '\n'.join(outstr)
+            lines.append("Current State Summations")
+            for lead, members in self._summations_index.items():
+                lines.append("\t{}={}".format(self._suminds[lead], "+".join(self._snames[j] for j in members)))
+        return "\n".join(lines)
 
     __str__ = __repr__
 
     def set_parameters(self, **kwargs):
-        pset = set(self._pnames)
-        for p in kwargs:
-            if p in pset:
-                if isinstance(kwargs[p], parameter):
-                    self.parameters[p] = kwargs[p]
-                    if not self.parameters[p].name:
-                        self.parameters[p].name = p
-                else:
-                    if self.parameters[p]:
-                        self.parameters[p].val = kwargs[p]
-                    else:
-                        self.parameters[p] = parameter(init_value=kwargs[p], name=p)
+        for name, value in kwargs.items():
+            if name not in self.parameters:
+                raise ValueError(f"unknown parameter {name!r}; this model's parameters are {', '.join(self._pnames)}")
+            if isinstance(value, parameter):
+                value.name = value.name or name
+                self.parameters[name] = value
+            elif self.parameters[name] is not None:
+                self.parameters[name].val = value  # keep the prior, move the value
             else:
-                raise Exception("{} is an unknown parameter. Acceptable parameters are: {}".format(
-                    p, ', '.join(self._pnames)))
+                self.parameters[name] = parameter(init_value=value, name=name)
 
     def set_inits(self, **kwargs):
-        s_set = set(self._snames)
-        ss_set = set(self._summation_snames)
-        for s in kwargs:
-            if s in s_set:
-                self.istates[s] = kwargs[s]
-            elif s in ss_set:
-                pass  # summed names are not initial conditions (Framework.py:476-477)
-            else:
-                raise Exception("{} is an unknown state variable. Acceptable parameters are: {}".format(
-                    s, ', '.join(self._snames)))
+        for name, value in kwargs.items():
+            if name in self.istates:
+                self.istates[name] = value
+            elif name not in self._summation_snames:  # a summed column is not a state (Framework.py:476-477)
+                raise ValueError(f"unknown state variable {name!r}; this model's states are {', '.join(self._snames)}")
 
     def get_inits(self, as_dict=False):
         if as_dict:
             return self.istates
-        return np.array([self.istates[el] for el in self._snames])
+        return np.array([self.istates[s] for s in self._snames])
 
     def get_model(self):
         return self._model
 
     def get_parameters(self, as_dict=False, **kwargs):
-        if as_dict:
-            return {p: (kwargs[p] if p in kwargs else self.parameters[p].val) for p in self.get_pnames()}
-        ps = [kwargs[p] if p in kwargs else self.parameters[p].val for p in self.get_pnames()]
-        return tuple([ps])
+        vals = {p: (kwargs[p] if p in kwargs else self.parameters[p].val) for p in self._pnames}
+        return vals if as_dict else (list(vals.values()),)
 
     def get_numstatevar(self):
         return len(self._snames)
@@ -339,10 +280,7 @@ class ModelFramework:
         """Observations in get_chi's concatenation order (Framework.py:685-697): the
         integrate() mod_dict order = post-summation state order, states with data."""
         out_names = self.get_snames(after_summation=True)
-        cols = []
-        for i, sname in enumerate(out_names):
-            if sname in self._pred_tindex:
-                cols.append((sname, i))
+        cols = [(sname, i) for i, sname in enumerate(out_names) if sname in self._pred_tindex]
         keep = self._sumkeep if self._summations_index else tuple(range(len(self._snames)))
         return out_names, cols, keep
 
@@ -356,13 +294,13 @@ class ModelFramework:
         sstot = 0
         for sname, ci in cols:
             orig = keep[ci]
-            group = self._summations_index.get(orig, (orig,)) if self._summations_index else (orig,)
-            m = 0
+            group = self._summations_index.get(orig, (orig,))
+            bits = 0
             for s in group:
-                m |= (1 << s)
+                bits |= (1 << s)
             n = len(self._pred_tindex[sname])
             tidx.append(np.asarray(self._pred_tindex[sname], np.int32))
-            mask.append(np.full(n, m, np.uint64))
+            mask.append(np.full(n, bits, np.uint64))
             O.append(np.asarray(self._obs_logabundance[sname], float))
             Ssig.append(np.asarray(self._obs_logsigma[sname], float))
             olin = np.exp(self._obs_logabundance[sname])  # Framework.py:700
@@ -430,26 +368,21 @@ class ModelFramework:
         ps = [float(np.asarray(v)) for v in ps[0]]
         res = self.integrate_batch([ps], inits=[np.asarray(initials, float)], trajectory=True)
         mod = res["traj"][:, :, 0].cpu().numpy().copy()
-        if sum_subpopulations and self._summations_index:
-            for sumi in self._summations_index:
-                mod[:, sumi] = mod[:, self._summations_index[sumi]].sum(axis=1)
-            mod = mod[:, self._sumkeep]
+        if sum_subpopulations:
+            mod = datasetup.apply_summations(mod, self._summation_plan)
+        names = self.get_snames(after_summation=sum_subpopulations)
         if as_dataframe:
-            df = pd.DataFrame(mod)
-            df.columns = self.get_snames(after_summation=sum_subpopulations)
+            df = pd.DataFrame(mod, columns=names)
             df['time'] = self.times
-            if predict_obs:
-                calc = pd.melt(df[self.get_snames(predict_obs=True) + ['time']], id_vars=['time'])
-                calc.columns = ['time', 'organism', 'abundance']
-                calc = calc.set_index('organism')
-                return pd.concat([calc.loc[s].iloc[self._pred_tindex[s]] for s in self.get_snames(predict_obs=True)])
-            return df
+            if not predict_obs:
+                return df
+            observed = self.get_snames(predict_obs=True)
+            long = pd.melt(df[observed + ['time']], id_vars=['time'])
+            long.columns = ['time', 'organism', 'abundance']
+            long = long.set_index('organism')
+            return pd.concat([long.loc[s].iloc[self._pred_tindex[s]] for s in observed])
         if predict_obs:
-            mod_dict = {}
-            for i, sname in enumerate(self.get_snames(after_summation=sum_subpopulations)):
-                if sname in self._pred_tindex:
-                    mod_dict[sname] = mod[:, i][self._pred_tindex[sname]]
-            return mod_dict
+            return {s: mod[:, i][self._pred_tindex[s]] for i, s in enumerate(names) if s in self._pred_tindex}
         return mod
 
     def get_residuals(self):
@@ -458,179 +391,183 @@ class ModelFramework:
 
     # ------------------------------------------------------------------ fit statistics
     def get_chi(self, mod_dict):
-        O, Cc, S = [], [], []
-        for sname in mod_dict:
-            O.append(self._obs_logabundance[sname])
-            Cc.append(np.log(mod_dict[sname]))
-            S.append(self._obs_logsigma[sname])
-        return stats.chi(O=np.concatenate(O, axis=0), C=np.concatenate(Cc, axis=0), S=np.concatenate(S, axis=0))
+        """stats.chi over the observed columns in ``mod_dict``'s order (Framework.py:685-697)."""
+        names = list(mod_dict)
+        return stats.chi(O=np.concatenate([self._obs_logabundance[s] for s in names], axis=0),
+                         C=np.concatenate([np.log(mod_dict[s]) for s in names], axis=0),
+                         S=np.concatenate([self._obs_logsigma[s] for s in names], axis=0))
 
     def get_Rsqrd(self, mod_dict):
-        abundance_dict = {el: np.exp(self._obs_logabundance[el]) for el in self._obs_logabundance}
-        return stats.Rsqrd(C_dict=mod_dict, O_dict=abundance_dict)
+        observed = {s: np.exp(v) for s, v in self._obs_logabundance.items()}
+        return stats.Rsqrd(C_dict=mod_dict, O_dict=observed)
 
     def get_AIC(self, chi):
         return stats.AIC(chi, self._pnum)
 
     def get_adjRsqrd(self, mod_dict, Rsqrd=None):
-        if not Rsqrd:
-            Rsqrd = self.get_Rsqrd(mod_dict)
-        return stats.get_adjusted_rsquared(Rsqrd, self._samples, self._pnum)
+        r2 = Rsqrd if Rsqrd else self.get_Rsqrd(mod_dict)
+        return stats.get_adjusted_rsquared(r2, self._samples, self._pnum)
 
     def get_fitstats(self, prediction_dict=dict()):
-        fs = {}
-        if not prediction_dict:
-            prediction_dict = self.integrate(predict_obs=True, as_dataframe=False)
-        fs['Chi'] = self.get_chi(prediction_dict)
-        fs['R^2'] = self.get_Rsqrd(prediction_dict)
-        fs['AIC'] = self.get_AIC(fs['Chi'])
-        return fs
+        pred = prediction_dict if prediction_dict else self.integrate(predict_obs=True, as_dataframe=False)
+        chi = self.get_chi(pred)
+        return {'Chi': chi, 'R^2': self.get_Rsqrd(pred), 'AIC': self.get_AIC(chi)}
 
     def set_best_params(self, posteriors):
-        im = posteriors.loc[posteriors.chi == min(posteriors.chi)].index[0]
-        bestchain = posteriors.iloc[im]["chain#"]
-        posteriors = posteriors[posteriors["chain#"] == bestchain]
-        self.set_parameters(**posteriors.loc[im][self.get_pnames()].to_dict())
-        if self._snames[0] + '0' in self.get_pnames():
-            self.set_inits(**{o: posteriors.loc[im][self.get_pnames()].to_dict()[o + '0'] for o in self._snames})
+        """Move the model to the posterior row with the lowest chi (the first such row;
+        Framework.py:725-731), '<state>0' parameters included."""
+        best = posteriors.iloc[int(np.nanargmin(posteriors['chi'].to_numpy(dtype=float)))]
+        values = best[self.get_pnames()].to_dict()
+        self.set_parameters(**values)
+        if self._snames[0] + '0' in values:
+            self.set_inits(**{s: values[s + '0'] for s in self._snames if s + '0' in values})
 
     def plot_uncertainty(self, ax, posteriors, variable, ntimes=100):
-        for a in range(ntimes):
-            im = rd.choice(posteriors.index)
-            self.set_inits(**{o: posteriors.loc[im][self.get_pnames()].to_dict()[o + '0'] for o in self._snames})
-            self.set_parameters(**posteriors.loc[im][self.get_pnames()].to_dict())
-            mod = self.integrate()
-            ax.plot(mod.time, mod[variable], c=str(0.8), lw=1, zorder=1)
+        """Overlay ``ntimes`` trajectories of random posterior rows (Framework.py:734-740)."""
+        for _ in range(ntimes):
+            row = posteriors.loc[random.choice(posteriors.index)][self.get_pnames()].to_dict()
+            self.set_inits(**{s: row[s + '0'] for s in self._snames})
+            self.set_parameters(**row)
+            traj = self.integrate()
+            ax.plot(traj.time, traj[variable], c=str(0.8), lw=1, zorder=1)
 
     # ------------------------------------------------------------------ LHS survey
     def _lhs_samples(self, samples=100, **kwargs):
-        pdists, pstatic = {}, {}
+        """LHS draws through the priors; parameters without a prior (and not remapped in
+        ``kwargs``) keep their value (Framework.py:589-615)."""
+        drawn = {p: kwargs.get(p, self.parameters[p]) for p in self.parameters
+                 if p in kwargs or self.parameters[p].has_distribution()}
+        df = Samplers.sample_lhs(parameter_dict=drawn, samples=samples)
         for p in self.parameters:
-            if p in kwargs:
-                pdists[p] = kwargs[p]
-            elif self.parameters[p].has_distribution():
-                pdists[p] = self.parameters[p]
-            else:
-                pstatic[p] = self.parameters[p].val
-        df = Samplers.sample_lhs(parameter_dict=pdists, samples=samples)
-        for p in pstatic:
-            df[p] = pstatic[p]
+            if p not in drawn:
+                df[p] = self.parameters[p].val
         return df
 
     def fit_survey(self, samples=1000, cpu_cores=1):
         """LHS draws through the priors, then ONE batched integrate+chi launch over all
-        samples (Framework.py:800-816; the per-sample loop of _Fit_worker :41-48)."""
-        ps = self._lhs_samples(samples)
-        ps = ps[self.get_pnames()]
+        samples (Framework.py:800-816; the per-sample loop of _Fit_worker :41-48).  Rows
+        come back in the order and with the index the reference's ``cpu_cores`` workers
+        produce; the likelihood of a sample whose every term is masked is NaN."""
+        ps = self._lhs_samples(samples)[self.get_pnames()]
         res = self.integrate_batch(ps.to_numpy(dtype=float), trajectory=False)
-        out = ps.copy().reset_index(drop=True)
+        out = ps.reset_index(drop=True)
         out['chi'] = res["chi"].cpu().numpy()
+        order, index = _worker_order(len(out), cpu_cores)
+        out = out.iloc[order]
+        out.index = index
         return out
 
     def explore_equilibriums(self, samples=1000, cpu_cores=1, **parameter_mapping):
-        """final state of each LHS sample (Framework.py:819-855), one batched launch"""
+        """Final state of each LHS sample (Framework.py:819-855), one batched launch."""
+        print("Sampling with a Latin Hypercube scheme")
         ps = self._lhs_samples(samples, **parameter_mapping)[self.get_pnames()]
         res = self.integrate_batch(ps.to_numpy(dtype=float), trajectory=True)
         final = res["traj"][-1].cpu().numpy().T  # [W][S]
         df = pd.DataFrame(final, columns=self.get_snames(after_summation=False))
         for p in self.get_pnames():
             df[p] = ps[p].to_numpy()
+        order, index = _worker_order(len(df), cpu_cores)
+        df = df.iloc[order]
+        df.index = index
         return df
 
     def copy(self, overwrite=dict()):
-        newmod = ModelFramework.__new__(ModelFramework)
+        clone = ModelFramework.__new__(ModelFramework)
         for attr, v in self.__dict__.items():
             if attr in ('parameters', '_engine'):
                 continue
-            if isinstance(v, (list, dict, pd.DataFrame, np.ndarray)):
-                newmod.__dict__[attr] = v.copy()
-            else:
-                newmod.__dict__[attr] = v
-        newmod.parameters = {p: (self.parameters[p].copy() if self.parameters[p] is not None else None)
-                             for p in self.parameters}
-        newmod._engine = self._engine  # shared context; engine() checks Engine.key before use
-        _ps = {el: overwrite[el] for el in overwrite if el in newmod._pnames}
-        _is = {el: overwrite[el] for el in overwrite if el in newmod._snames}
-        if _ps:
-            newmod.set_parameters(**_ps)
-        if _is:
-            newmod.set_inits(**_is)
-        return newmod
+            clone.__dict__[attr] = v.copy() if isinstance(v, (list, dict, pd.DataFrame, np.ndarray)) else v
+        clone.parameters = {p: (v.copy() if v is not None else None) for p, v in self.parameters.items()}
+        clone._engine = self._engine  # shared context; engine() checks Engine.key before use
+        new_ps = {k: v for k, v in overwrite.items() if k in clone._pnames}
+        new_is = {k: v for k, v in overwrite.items() if k in clone._snames}
+        if new_ps:
+            clone.set_parameters(**new_ps)
+        if new_is:
+            clone.set_inits(**new_is)
+        return clone
 
     # ------------------------------------------------------------------ MCMC
+    def _survey_chain_starts(self, n_chains, fitsurvey_samples, sd_fitdistance, cpu_cores):
+        """Chain starts for ``MCMC(chain_inits=<int>)`` (Framework.py:993-1012): survey the
+        priors, drop failed integrations, keep samples whose chi beats the chi of data
+        shifted by ``sd_fitdistance`` log sigmas, draw the starts from them with
+        replacement (pandas ``sample``: numpy's global RNG)."""
+        survey = self.fit_survey(samples=fitsurvey_samples, cpu_cores=cpu_cores).dropna()
+        if survey.empty:
+            warnings.warn("Pre-sampling of Multidimentional space failed")
+            return pd.DataFrame([[]] * n_chains)
+        shifted = {s: np.exp(self._obs_logabundance[s] + sd_fitdistance * self._obs_logsigma[s])
+                   for s in self._obs_logabundance}
+        good = survey[survey['chi'] < self.get_chi(shifted)]
+        if good.empty:
+            raise ValueError("the fit survey found no parameter set within sd_fitdistance of the data; "
+                             "increase sd_fitdistance or fitsurvey_samples, or revise the priors / initial values")
+        return good.sample(n_chains, replace=True)
+
     def MCMC(self, chain_inits=1, iterations_per_chain=1000, cpu_cores=1, static_parameters=list(),
-             print_report=True, fitsurvey_samples=1000, sd_fitdistance=3.0, rng='replay', seed=0):
+             print_report=True, fitsurvey_samples=1000, sd_fitdistance=3.0, rng='replay', seed=0,
+             print_iterations=True):
         """Markov chain Monte Carlo over all chains at once (Framework.py:946-1061).
 
         Each chain is one walker of a single batched ``oe_mh_run``; chain i keeps the
-        reference's seed i (Framework.py:1015/1020).  ``cpu_cores`` is accepted for
-        API compatibility and ignored."""
+        reference's seed i (Framework.py:1015/1020).  ``cpu_cores`` only shapes the fit
+        survey's row order, as the reference's workers would.  ``print_iterations``
+        (new): the reference's chains print ``it exp(-chi)`` on every iteration
+        (Samplers.py:123), chain after chain; pass False for large ensembles."""
         if isinstance(chain_inits, pd.DataFrame):
-            chain_inits = [row.to_dict() for i, row in chain_inits[self.get_pnames()].iterrows()]
+            chain_inits = [row.to_dict() for _, row in chain_inits[self.get_pnames()].iterrows()]
         if isinstance(chain_inits, int):
-            fitsurvey = self.fit_survey(samples=fitsurvey_samples)
-            fitsurvey.dropna(inplace=True)
-            if fitsurvey.empty:
-                initps = pd.DataFrame([[]] * chain_inits)
-                warnings.warn("Pre-sampling of Multidimentional space failed")
-            else:
-                calc = {s: np.exp(self._obs_logabundance[s] + sd_fitdistance * self._obs_logsigma[s])
-                        for s in self._obs_logabundance}
-                cutchi = self.get_chi(calc)
-                if sum(fitsurvey['chi'] < cutchi) == 0:
-                    raise ValueError("Preliminary sampling found no parameter sets which meet the minimal threshold \n"
-                                     " Try: 1. Increasing sd_fitdistance 2. Increasing fitsurvey_samples "
-                                     "3. Different priors and / or different parameter guesses")
-                initps = fitsurvey[fitsurvey['chi'] < cutchi].sample(chain_inits, replace=True)
-            chains = [self.copy(overwrite=initps.iloc[i].to_dict()) for i in range(chain_inits)]
-        else:
-            chains = [self.copy(overwrite=inits) for inits in chain_inits]
-        for i, m in enumerate(chains):
-            m.random_seed = i
+            starts = self._survey_chain_starts(chain_inits, fitsurvey_samples, sd_fitdistance, cpu_cores)
+            chain_inits = [starts.iloc[i].to_dict() for i in range(chain_inits)]
+        chains = [self.copy(overwrite=inits) for inits in chain_inits]
+        for i, c in enumerate(chains):
+            c.random_seed = i
+        print('working')
         posterior = Samplers.batched_metropolis_hastings(
             chains, nits=iterations_per_chain, burnin=int(iterations_per_chain / 2),
-            static_parameters=static_parameters, rng=rng, seed=seed, engine=self.engine())
+            static_parameters=static_parameters, rng=rng, seed=seed, engine=self.engine(),
+            iteration_log=print_iterations)
+        print('not working')
         if print_report:
-            report = ["\nFitting Report\n==============="]
-            for col in list(self.get_pnames()):
-                median, std = rawstats(posterior[col])
-                if (median != 0.0) and (std != 0.0):
-                    report.append("parameter: {}\n\tmedian = {:0.3e}, Standard deviation = {:0.3e}".format(
-                        col, median, std))
-            self.set_best_params(posterior)
-            mod = self.integrate(predict_obs=True, as_dataframe=False)
-            fs = self.get_fitstats(mod)
-            report.append("\nMedian parameter fit stats:")
-            report.append("\tChi = {:0.3e}\n\tR-squared = {:0.3e}\n\tAIC = {:0.3e}".format(
-                fs['Chi'], fs['R^2'], fs['AIC']))
-            print('\n'.join(report))
+            self._print_fit_report(posterior)
         return posterior
+
+    def _print_fit_report(self, posterior):
+        """The report MCMC prints (Framework.py:1047-1060)."""
+        lines = ["\nFitting Report\n==============="]
+        for p in self.get_pnames():
+            median, std = rawstats(posterior[p])
+            if median != 0.0 and std != 0.0:
+                lines.append("parameter: {}\n\tmedian = {:0.3e}, Standard deviation = {:0.3e}".format(p, median, std))
+        self.set_best_params(posterior)
+        fs = self.get_fitstats(self.integrate(predict_obs=True, as_dataframe=False))
+        lines.append("\nMedian parameter fit stats:")
+        lines.append("\tChi = {:0.3e}\n\tR-squared = {:0.3e}\n\tAIC = {:0.3e}".format(fs['Chi'], fs['R^2'], fs['AIC']))
+        print('\n'.join(lines))
 
     # ------------------------------------------------------------------ plotting
     def _calc_stds(self, state):
-        logabundance = self._obs_logabundance[state]
-        logstd = self._obs_logsigma[state]
-        low = np.exp(logabundance) - np.exp(logabundance - logstd)
-        high = np.exp(logabundance + logstd) - np.exp(logabundance)
-        return np.array([low, high])
+        """Asymmetric linear-space error bars of ±1 log sigma around the data."""
+        centre = self._obs_logabundance[state]
+        spread = self._obs_logsigma[state]
+        return np.array([np.exp(centre) - np.exp(centre - spread), np.exp(centre + spread) - np.exp(centre)])
 
     def plot(self, states=None, overlay=dict()):
         import matplotlib.pyplot as plt
-        if not states:
-            states = self.get_snames(predict_obs=True)
-        rplt = (len(states) % 2 + len(states)) / 2
-        f, ax = plt.subplots(int(rplt), 2, figsize=[9, 4.5])
-        ax = np.atleast_1d(ax).ravel()
-        mod = self.integrate()
-        for i, state in enumerate(states):
+        states = states or self.get_snames(predict_obs=True)
+        fig, axes = plt.subplots(int((len(states) + len(states) % 2) / 2), 2, figsize=[9, 4.5])
+        axes = np.atleast_1d(axes).ravel()
+        traj = self.integrate()
+        for ax, state in zip(axes, states):
             if state in self.df.index:
-                ax[i].errorbar(self.df.loc[state]['time'], self.df.loc[state]['abundance'],
-                               yerr=self._calc_stds(state))
-            ax[i].set_xlabel('Time')
-            ax[i].set_ylabel(state + ' ml$^{-1}$')
-            ax[i].semilogy()
-            if state in mod:
-                ax[i].plot(self.times, mod[state])
-                for el in overlay.get(state, []):
-                    ax[i].plot(self.times, mod[el])
-        return f, ax
+                obs = self.df.loc[state]
+                ax.errorbar(obs['time'], obs['abundance'], yerr=self._calc_stds(state))
+            ax.set_xlabel('Time')
+            ax.set_ylabel(state + ' ml$^{-1}$')
+            ax.semilogy()
+            if state in traj:
+                ax.plot(self.times, traj[state])
+                for other in overlay.get(state, []):
+                    ax.plot(self.times, traj[other])
+        return fig, axes

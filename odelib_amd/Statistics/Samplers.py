@@ -32,28 +32,28 @@ def lhs_classic(n, samples):
 
 
 def sample_lhs(parameter_dict, samples):
-    """LHS draws mapped through each prior's ppf (Samplers.py:6-51)."""
-    total_ps = 0
-    for p in parameter_dict:
-        total_ps += np.count_nonzero(parameter_dict[p].val)
-    lhd = lhs_classic(total_ps, samples=samples)
-    var_samples = {}
-    lhd_i = 0
-    for p in parameter_dict:
-        nump = np.count_nonzero(parameter_dict[p].val)
-        s = lhd[:, lhd_i:lhd_i + nump]
-        lhd_i += nump
-        s = parameter_dict[p].dist.ppf(s, **parameter_dict[p].hp)
-        if nump == 1:
-            var_samples[p] = np.concatenate(s, axis=None)
-        else:
-            _sample = []
-            _p = np.array(parameter_dict[p].val, dtype=float)
-            for row in s:
-                _p[np.where(_p != 0)] = row
-                _sample.append(np.copy(_p))
-            var_samples[p] = _sample
-    return pd.DataFrame(var_samples)
+    """Latin-hypercube samples of the parameters in ``parameter_dict`` (name -> parameter
+    with a prior), mapped through each prior's ppf (Samplers.py:6-51).  An array-valued
+    parameter takes one hypercube dimension per non-zero element and yields one array per
+    sample (its zero elements stay zero).  Returns a DataFrame with one column per name."""
+    width = {name: int(np.count_nonzero(par.val)) for name, par in parameter_dict.items()}
+    unit = lhs_classic(sum(width.values()), samples=samples)
+    columns, first = {}, 0
+    for name, par in parameter_dict.items():
+        block = par.dist.ppf(unit[:, first:first + width[name]], **par.hp)
+        first += width[name]
+        if width[name] == 1:
+            columns[name] = block.ravel()
+            continue
+        template = np.array(par.val, dtype=float)
+        slots = template != 0
+        rows = []
+        for draw in block:
+            row = template.copy()
+            row[slots] = draw
+            rows.append(row)
+        columns[name] = rows
+    return pd.DataFrame(columns)
 
 
 def _posterior_frame(samples, pnames, static_parameters, chains, kept):
@@ -81,12 +81,40 @@ def _posterior_frame(samples, pnames, static_parameters, chains, kept):
     return out
 
 
+def _fmt(x):
+    """How the reference's print shows a likelihood value: str of an np.float64, or '--'
+    for an all-masked chi (np.ma.masked, NaN here)."""
+    return "--" if np.isnan(x) else str(np.float64(x))
+
+
+def _print_iterations(a_priori, chi_rows):
+    """The line every reference chain prints on every iteration, before its decision
+    (Samplers.py:123: ``print(it, np.exp(-chi))`` with chi the current state's):
+    iteration 1 shows the a-priori chi, iteration it the chi after iteration it-1.
+    a_priori [W], chi_rows [nits-1][W] (chain state after each iteration); chain after
+    chain, as the reference's serial MCMC loop prints them."""
+    import sys
+    n, W = chi_rows.shape
+    with np.errstate(over="ignore", invalid="ignore"):
+        for w in range(W):
+            prev = np.concatenate([[a_priori[w]], chi_rows[:-1, w]]) if n else np.zeros(0)
+            err = np.exp(-prev)
+            sys.stdout.write("".join(f"{it} {_fmt(e)}\n" for it, e in zip(range(1, n + 1), err)))
+    sys.stdout.flush()
+
+
 def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameters=(), rng="replay", seed=0,
-                                engine=None, walker_offset=0, return_device=False):
+                                engine=None, walker_offset=0, return_device=False, iteration_log=False,
+                                print_prior=False):
     """Run ``len(chains)`` Metropolis–Hastings chains as walkers of one device launch.
 
     chains : ModelFramework copies (one per chain, each with its own initial θ,
-             initial states and ``random_seed``); they must share the fit problem."""
+             initial states and ``random_seed``); they must share the fit problem.
+    iteration_log : print the reference's per-iteration line of every chain (the run
+             then keeps every iteration's row on the device and drops the burn-in rows
+             on the host: same chains, the kernel's arithmetic does not depend on burnin).
+    print_prior : print the reference's ``a priori error`` line and header first
+             (MetropolisHastings with print_progress, Samplers.py:101-103)."""
     m0 = chains[0]
     pnames = m0.get_pnames()
     snames = list(m0._snames)
@@ -94,6 +122,7 @@ def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameter
     if not burnin:
         burnin = int(nits / 2)
     W = len(chains)
+    P = len(pnames)
     theta = np.array([[float(np.asarray(c.parameters[p].val)) for p in pnames] for c in chains]).T.copy()
     y0 = np.array([[float(np.asarray(c.istates[s])) for s in snames] for c in chains]).T.copy()
     walk = [p not in reject for p in pnames]
@@ -112,32 +141,39 @@ def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameter
         else:
             rng = "replay"
             replay = legacy_replay_streams(seeds, nits, pnames, walking, dists, oldvals=theta.T.tolist())
-    res = eng.mh_run(theta, y0, nits=nits, burnin=burnin, walk_mask=walk, init_param=init_param, rng=rng,
-                     seed=seed, replay=replay, walker_offset=walker_offset, numpy_seeds=numpy_seeds,
-                     prior_draws=prior_draws)
+    kw = dict(walk_mask=walk, init_param=init_param, rng=rng, seed=seed, replay=replay, walker_offset=walker_offset,
+              numpy_seeds=numpy_seeds, prior_draws=prior_draws)
+    logging = (iteration_log or print_prior) and not return_device
+    a_priori = None
+    if logging:  # the a-priori state's chi: the kernel's own first integration (nits = 1)
+        a_priori = eng.mh_run(theta, y0, nits=1, burnin=0, **kw)["final"][0].cpu().numpy()
+    res = eng.mh_run(theta, y0, nits=nits, burnin=0 if iteration_log and not return_device else burnin, **kw)
     kept = max(0, nits - 1 - burnin)
     if return_device:
         return res
-    samples = res["samples"].cpu().numpy() if kept > 0 else None
+    if print_prior:
+        print('a priori error', _fmt(a_priori[0]) if W == 1 else a_priori)
+        print('iteration; error; acceptance ratio')
+    samples = res["samples"].cpu().numpy() if res["samples"].shape[0] > 0 else None
+    if iteration_log:
+        _print_iterations(a_priori, samples[:, P, :] if samples is not None else np.zeros((0, W)))
+        samples = samples[burnin:] if (samples is not None and kept > 0) else None
     th = res["theta"].cpu().numpy()
     yf = res["y0"].cpu().numpy()
     for w, c in enumerate(chains):  # chains end at their last state, as the reference leaves them
         c.set_parameters(**{p: th[j, w] for j, p in enumerate(pnames) if p not in reject})
         c.set_inits(**{s: yf[k, w] for k, s in enumerate(snames)})
-    return _posterior_frame(samples, pnames, static_parameters, chains, kept)
+    return _posterior_frame(samples if kept > 0 else None, pnames, static_parameters, chains, kept)
 
 
 def MetropolisHastings(modelframework, nits=1000, burnin=None, static_parameters=set(), print_progress=True):
-    """Single-chain drop-in of Samplers.MetropolisHastings (Samplers.py:53-174), on
-    the device, with the reference's numpy draws replayed (seed = random_seed)."""
+    """Single-chain drop-in of Samplers.MetropolisHastings (Samplers.py:53-174), on the
+    device, with the reference's numpy draws replayed (seed = random_seed).  Prints what
+    the reference prints: with ``print_progress`` the a-priori chi and a header, and on
+    every iteration ``it exp(-chi)`` (Samplers.py:101-103, :123)."""
     if not burnin:
         burnin = int(nits / 2)
     df = batched_metropolis_hastings([modelframework], nits=nits, burnin=burnin,
-                                     static_parameters=static_parameters, rng="replay")
-    df = df.drop(columns=["chain#"])
-    if print_progress:
-        print("iteration; error; acceptance ratio")
-        if len(df) and "chi" in df:
-            print(int(df["iteration"].iloc[-1]), float(np.exp(-df["chi"].iloc[-1])),
-                  float(df["acceptance_ratio"].iloc[-1]))
-    return df
+                                     static_parameters=static_parameters, rng="replay",
+                                     iteration_log=True, print_prior=print_progress)
+    return df.drop(columns=["chain#"])

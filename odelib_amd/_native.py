@@ -15,7 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ODELIB_AMD_LIB", os.path.join(_HERE, "csrc", "libodelib_amd.so"))
 
 # --- constants mirrored from include/odelib_amd.h -----------------------------------
-OE_ABI_VERSION = 3
+OE_ABI_VERSION = 4
+OE_COMM_ID_BYTES = 128
 OE_OK = 0
 OE_ERR_ARG, OE_ERR_HIP, OE_ERR_STATE, OE_ERR_UNSUPPORTED, OE_ERR_NOMEM = -1, -2, -3, -4, -5
 OE_METHOD_RK4, OE_METHOD_DOPRI5, OE_METHOD_AUTO, OE_METHOD_ROSENBROCK = 0, 1, 2, 3
@@ -42,6 +43,12 @@ EXPORTED = (
     "oe_mh_run",
     "oe_numpy_streams",
     "oe_last_kernel_ms",
+    "oe_comm_unique_id",
+    "oe_comm_init",
+    "oe_comm_destroy",
+    "oe_comm_last_error",
+    "oe_comm_set_stream",
+    "oe_allgather_samples",
 )
 
 
@@ -153,6 +160,18 @@ def load_library(path: str | None = None):
         lib.oe_numpy_streams.argtypes = [vp, i64, vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_double, vp, vp]
         lib.oe_last_kernel_ms.restype = C.c_int
         lib.oe_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+        lib.oe_comm_unique_id.restype = C.c_int
+        lib.oe_comm_unique_id.argtypes = [vp, i32]
+        lib.oe_comm_init.restype = C.c_int
+        lib.oe_comm_init.argtypes = [i32, i32, i32, vp, i32, C.POINTER(vp)]
+        lib.oe_comm_destroy.restype = None
+        lib.oe_comm_destroy.argtypes = [vp]
+        lib.oe_comm_last_error.restype = C.c_char_p
+        lib.oe_comm_last_error.argtypes = [vp]
+        lib.oe_comm_set_stream.restype = C.c_int
+        lib.oe_comm_set_stream.argtypes = [vp, vp]
+        lib.oe_allgather_samples.restype = C.c_int
+        lib.oe_allgather_samples.argtypes = [vp, i64, vp, vp, vp, u32]
         if lib.oe_abi_version() != OE_ABI_VERSION:
             raise NativeUnavailable("libodelib_amd.so ABI version mismatch; rebuild it")
         if path is None:
@@ -234,6 +253,58 @@ class Context:
     def close(self):
         if self._h and self._h.value:
             self.lib.oe_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (128 bytes) for ``Comm``: made on rank 0, handed to every rank."""
+    lib = load_library()
+    buf = (C.c_uint8 * OE_COMM_ID_BYTES)()
+    rc = lib.oe_comm_unique_id(C.cast(buf, C.c_void_p), OE_COMM_ID_BYTES)
+    if rc != OE_OK:
+        raise RuntimeError(f"oe_comm_unique_id failed ({rc}): {lib.oe_comm_last_error(None).decode()}")
+    return bytes(buf)
+
+
+class Comm:
+    """An RCCL communicator of the C-ABI (oe_comm): one rank per GPU, used to pool the
+    ranks' posterior sample blocks with ``oe_allgather_samples`` (Framework.py:1037)."""
+
+    def __init__(self, device: int, n_ranks: int, rank: int, unique_id: bytes):
+        self.lib = load_library()
+        if len(unique_id) != OE_COMM_ID_BYTES:
+            raise ValueError("unique_id must be 128 bytes")
+        buf = (C.c_uint8 * OE_COMM_ID_BYTES).from_buffer_copy(unique_id)
+        h = C.c_void_p()
+        rc = self.lib.oe_comm_init(int(device), int(n_ranks), int(rank), C.cast(buf, C.c_void_p), OE_COMM_ID_BYTES,
+                                   C.byref(h))
+        if rc != OE_OK:
+            raise RuntimeError(f"oe_comm_init failed ({rc}): {self.lib.oe_comm_last_error(None).decode()}")
+        self._h = h
+        self.device, self.n_ranks, self.rank = int(device), int(n_ranks), int(rank)
+
+    def set_stream(self, stream_handle: int):
+        self.lib.oe_comm_set_stream(self._h, C.c_void_p(int(stream_handle)))
+
+    def allgather_samples(self, rows: int, block_ptr, counts, out_ptr, flags: int = 0):
+        import numpy as np
+        cnt = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
+        if len(cnt) != self.n_ranks:
+            raise ValueError("counts must have one entry per rank")
+        rc = self.lib.oe_allgather_samples(self._h, int(rows), block_ptr, C.c_void_p(cnt.ctypes.data), out_ptr,
+                                           int(flags))
+        if rc != OE_OK:
+            raise RuntimeError(f"oe_allgather_samples failed ({rc}): {self.lib.oe_comm_last_error(self._h).decode()}")
+
+    def close(self):
+        if self._h and self._h.value:
+            self.lib.oe_comm_destroy(self._h)
             self._h = C.c_void_p()
 
     def __del__(self):  # pragma: no cover

@@ -51,6 +51,36 @@ def allgather_walkers(block, n_total: int, group=None):
     return torch.cat(parts, dim=-1)
 
 
+def native_comm(device: int, group=None):
+    """The C-ABI's RCCL communicator (``oe_comm``) over the ranks of a torch.distributed
+    group: rank 0 makes the id, one broadcast hands it to the others.  Without torch a
+    caller does the same with any channel."""
+    import torch.distributed as dist
+    from . import _native as N
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    obj = [N.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    return N.Comm(device, world, rank, obj[0])
+
+
+def native_allgather_walkers(block, n_total: int, comm):
+    """``allgather_walkers`` through ``oe_allgather_samples``: per-rank device blocks
+    [..., count_r] (walker axis last) pooled into [..., n_total] in global walker order."""
+    import torch
+    counts = [shard(n_total, r, comm.n_ranks)[1] for r in range(comm.n_ranks)]
+    if block.shape[-1] != counts[comm.rank]:
+        raise ValueError("block walker count does not match this rank's shard")
+    if block.device.type != "cuda" or block.dtype != torch.float64:
+        raise ValueError("oe_allgather_samples takes float64 device tensors")
+    blk = block.contiguous()
+    lead = tuple(blk.shape[:-1])
+    rows = int(np.prod(lead)) if lead else 1
+    out = torch.empty(lead + (int(n_total),), dtype=torch.float64, device=blk.device)
+    comm.set_stream(torch.cuda.current_stream(blk.device).cuda_stream)
+    comm.allgather_samples(rows, blk.data_ptr(), counts, out.data_ptr())
+    return out
+
+
 def sharded_mh(engine, theta_all, y0_all, nits: int, burnin: int, walk_mask, init_param=None, seed: int = 0,
                step_sd: float = 0.05, group=None):
     """Run the global ensemble ``theta_all [P][W_total]`` sharded over the ranks of

@@ -264,8 +264,11 @@ def metropolis_hastings(model: Model, nits=1000, burnin=None, static_parameters=
     acceptance uniforms come from the arrays instead of the global numpy RNG (and the
     prior ``rvs`` draws, whose values are unused at Samplers.py:118-121, are skipped).
     Returns a dict of columns: pnames..., chi, rsquared, aic, iteration,
-    acceptance_ratio, plus 'accepted' (per-iteration decisions, all iterations) and
-    'margin' (acc - u per iteration, for borderline analysis)."""
+    acceptance_ratio, plus 'accepted' (per-iteration decisions, all iterations),
+    'margin' (acc - u per iteration, for borderline analysis), 'a_priori' (the initial
+    chi, printed as 'a priori error') and 'printed' (the value the reference prints on
+    every iteration, exp(-chi) of the current state before the decision, Samplers.py:123;
+    NaN where it prints a masked value)."""
     if replay is None:
         np.random.seed(model.random_seed)
     pnames = model.get_pnames()
@@ -280,7 +283,8 @@ def metropolis_hastings(model: Model, nits=1000, burnin=None, static_parameters=
     rsq = model.get_Rsqrd(modcalc)
     aic_v = model.get_AIC(chi_v)
     rows, chis, its, rsqs, aics, ars_out = [], [], [], [], [], []
-    ars, accepted, margins = [], [], []
+    ars, accepted, margins, printed = [], [], [], []
+    a_priori = float(np.ma.filled(chi_v, np.nan)) if np.ma.is_masked(chi_v) else float(chi_v)
     pidx = {p: i for i, p in enumerate(pnames)}
     for it in iterations:
         for p in oldpar:
@@ -299,6 +303,8 @@ def metropolis_hastings(model: Model, nits=1000, burnin=None, static_parameters=
         if replay is None:
             [model.parameters[p].pdf(oldpar[p]) for p in oldpar]
             [model.parameters[p].pdf() for p in oldpar]
+        shown = np.exp(-chi_v)
+        printed.append(float(np.ma.filled(shown, np.nan)) if np.ma.is_masked(shown) else float(shown))
         lr = np.exp(chi_v - chinew)
         acc = np.exp(np.log(lr))
         u = np.random.rand() if replay is None else replay[1][it - 1]
@@ -333,5 +339,6 @@ def metropolis_hastings(model: Model, nits=1000, burnin=None, static_parameters=
         out[p] = np.full(len(rows), model.parameters[p].hp["scale"], dtype=float)
     out.update(chi=np.array(chis, float), rsquared=np.array(rsqs, float), aic=np.array(aics, float),
                iteration=np.array(its, float), acceptance_ratio=np.array(ars_out, float),
-               accepted=np.array(accepted, bool), margin=np.array(margins, float))
+               accepted=np.array(accepted, bool), margin=np.array(margins, float), a_priori=a_priori,
+               printed=np.array(printed, float))
     return out

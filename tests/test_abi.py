@@ -58,6 +58,17 @@ def test_errors_are_codes_not_crashes():
     assert lib.oe_last_kernel_ms(None, C.byref(ms)) == -1
     s, p = C.c_int32(0), C.c_int32(0)
     assert lib.oe_model_info(99, C.byref(s), C.byref(p)) == -4
+    # the pooling entry points validate before touching RCCL or the device
+    h = C.c_void_p()
+    uid = (C.c_uint8 * 128)()
+    assert lib.oe_comm_init(0, 0, 0, C.cast(uid, C.c_void_p), 128, C.byref(h)) == -1  # n_ranks < 1
+    assert lib.oe_comm_init(0, 2, 2, C.cast(uid, C.c_void_p), 128, C.byref(h)) == -1  # rank out of range
+    assert lib.oe_comm_init(0, 1, 0, C.cast(uid, C.c_void_p), 64, C.byref(h)) == -1   # wrong id size
+    assert b"rank" in lib.oe_comm_last_error(None)
+    assert lib.oe_comm_unique_id(None, 128) == -1
+    assert lib.oe_allgather_samples(None, 1, None, None, None, 0) == -1
+    assert lib.oe_comm_set_stream(None, None) == -1
+    lib.oe_comm_destroy(None)
 
 
 def test_context_creation_reports_missing_device():

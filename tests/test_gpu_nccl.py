@@ -51,6 +51,13 @@ CHILD = textwrap.dedent(r"""
         # the all-gather itself, with a ragged walker axis
         blk = torch.arange(W, dtype=torch.float64, device=dev).repeat(2, 1)
         assert torch.equal(allgather_walkers(blk, W), blk)
+        # the same pooling through the C-ABI's own RCCL communicator (oe_allgather_samples)
+        from odelib_amd.distributed import native_allgather_walkers, native_comm
+        comm = native_comm(0)
+        got = native_allgather_walkers(ref["samples"], W, comm)
+        assert got.device.type == "cuda" and torch.equal(got, ref["samples"])
+        assert torch.equal(native_allgather_walkers(blk, W, comm), blk)
+        comm.close()
         # pooled rawstats over RCCL == rawstats of the same posterior (Framework.py:11-17)
         med, std = pooled_rawstats(ref["samples"], P)
         s = ref["samples"].cpu().numpy()
@@ -70,6 +77,53 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+CABI_CHILD = textwrap.dedent(r"""
+    # the ODElib-side binding of INTEGRATION.md §4, without torch.distributed: ctypes
+    # only, one rank; the block is an MH posterior [kept][P+5][W] from oe_mh_run
+    import ctypes as C, os, sys
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(os.environ["ROOT"], "tests"))
+    sys.path.insert(0, os.environ["ROOT"])
+    from helpers import product_model
+    from odelib_amd import _native as N
+    m = product_model("two_i", method="rk4")
+    eng = m.engine()
+    W = 301
+    theta = np.repeat(np.array([float(m.parameters[p].val) for p in m.get_pnames()])[:, None], W, axis=1)
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    r = eng.mh_run(theta, y0, nits=9, burnin=3, walk_mask=np.ones(5, np.uint8), rng="philox", seed=2)
+    blk = r["samples"].contiguous()
+    rows = blk.numel() // W
+    lib = N.load_library()
+    uid = (C.c_uint8 * 128)()
+    assert lib.oe_comm_unique_id(C.cast(uid, C.c_void_p), 128) == 0
+    h = C.c_void_p()
+    assert lib.oe_comm_init(0, 1, 0, C.cast(uid, C.c_void_p), 128, C.byref(h)) == 0, lib.oe_comm_last_error(None)
+    out = torch.full_like(blk, float("nan"))
+    counts = np.array([W], np.int64)
+    rc = lib.oe_allgather_samples(h, rows, C.c_void_p(blk.data_ptr()), C.c_void_p(counts.ctypes.data),
+                                  C.c_void_p(out.data_ptr()), 0)
+    assert rc == 0, lib.oe_comm_last_error(h)
+    assert torch.equal(out, blk)
+    assert lib.oe_allgather_samples(h, -1, None, C.c_void_p(counts.ctypes.data), None, 0) == N.OE_ERR_ARG
+    assert lib.oe_allgather_samples(h, rows, None, C.c_void_p(counts.ctypes.data), C.c_void_p(out.data_ptr()),
+                                    N.OE_HOST_PTRS) == N.OE_ERR_ARG
+    lib.oe_comm_destroy(h)
+    print("CABI OK")
+""")
+
+
+@pytest.mark.gpu
+def test_rccl_world1_allgather_through_the_c_abi():
+    """oe_comm_unique_id / oe_comm_init / oe_allgather_samples bound with ctypes alone (no
+    torch.distributed): a world-size-1 RCCL communicator pools the MH posterior block."""
+    env = dict(os.environ, ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", CABI_CHILD], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0 and "CABI OK" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
 
 
 @pytest.mark.gpu

@@ -13,6 +13,7 @@
   moves acc by ~1e-5).
 """
 import numpy as np
+import pandas as pd
 import pytest
 
 from helpers import CONFIGS, THETA, chain_problem, oracle_model, product_model, walker_thetas
@@ -451,10 +452,38 @@ def test_dropin_metropolis_hastings_vs_reference_chain(golden, key):
     assert list(post.columns) == meta["columns"]
     burnin = meta["nits"] // 2
     rows = max(0, n_ok - burnin)  # kept rows fully decided by decisive iterations
-    assert rows > 0
+    # every acceptance of these chains is decisive (|acc - u| > 1e-3), so every kept row
+    # is compared — the bound is stated, not just "some rows"
+    assert rows == meta["nits"] - 1 - burnin == len(post)
     for c in meta["columns"]:
         np.testing.assert_allclose(post[c].to_numpy(dtype=float)[:rows], golden.mh[f"{key}/{c}"][:rows],
                                    rtol=2e-5, err_msg=c)
+
+
+@pytest.mark.parametrize("key", ["one_i_s7", "zero_i_s0_static"])
+def test_dropin_metropolis_hastings_prints_the_reference_progress(golden, capsys, key):
+    """What the reference prints (Samplers.py:101-103, :123): 'a priori error <chi>', the
+    header, then ``it exp(-chi)`` on every iteration (chi of the current state before the
+    decision) — line for line, values to the integration accuracy (rtol 2e-5, as the
+    posterior rows)."""
+    from odelib_amd.Statistics import Samplers
+    meta = golden.meta[f"mh/{key}"]
+    om = oracle_model(meta["model"], seed=meta["seed"], extra_params=meta["extra"] or None)
+    ref = cpu_ref.metropolis_hastings(om, nits=meta["nits"], static_parameters=meta["static"])
+    m = product_model(meta["model"], seed=meta["seed"], extra_params=meta["extra"] or None, rtol=1e-10, atol=1e-10)
+    Samplers.MetropolisHastings(m, nits=meta["nits"], static_parameters=set(meta["static"]), print_progress=True)
+    lines = capsys.readouterr().out.strip().splitlines()
+    head, chi0 = lines[0].rsplit(" ", 1)
+    assert head == "a priori error" and lines[1] == "iteration; error; acceptance ratio"
+    np.testing.assert_allclose(float(chi0), ref["a_priori"], rtol=2e-5)
+    body = [ln.split() for ln in lines[2:]]
+    assert [int(b[0]) for b in body] == list(range(1, meta["nits"]))
+    got = np.array([float(b[1]) for b in body])
+    np.testing.assert_allclose(got, ref["printed"], rtol=2e-5)
+    # MCMC's chains print the same per-iteration lines (print_progress=False there)
+    Samplers.MetropolisHastings(m.copy(), nits=5, print_progress=False)
+    quiet = capsys.readouterr().out.strip().splitlines()
+    assert [q.split()[0] for q in quiet] == ["1", "2", "3", "4"]
 
 
 def _ulps(a, b):
@@ -556,6 +585,7 @@ def test_dropin_mcmc_vs_reference(golden, capsys):
         om = oracle_model("one_i", theta=init, seed=i)
         n_ok = _decisive_prefix(cpu_ref.metropolis_hastings(om, nits=nits)["margin"])
         rows = max(0, n_ok - nits // 2)
+        assert rows == nits - 1 - nits // 2  # all kept rows of every chain are compared
         sel = golden.mcmc["post/chain#"] == i
         mine = post[post["chain#"] == i]
         for c in meta["columns"]:
@@ -563,17 +593,100 @@ def test_dropin_mcmc_vs_reference(golden, capsys):
                                        rtol=2e-5, err_msg=f"chain {i} {c}")
 
 
-def test_fit_survey_and_equilibria():
+def _oracle_chi(name, rows, tight=False):
+    """The reference's per-sample chi (_Fit_worker, Framework.py:41-48): odeint + the
+    masked chi of get_chi; NaN where every term is masked."""
+    om = oracle_model(name)
+    y0 = [om.istates[s] for s in CONFIGS[name]["snames"]]
+    tol = dict(rtol=1e-13, atol=1e-13) if tight else {}
+    out = []
+    for row in rows:
+        tr = cpu_ref.odeint_traj(RHS[name], y0, om.times, row, **tol)
+        om.integrator = lambda y, ps, tr=tr: tr
+        c = om.get_chi(om.integrate_obs())
+        out.append(np.nan if np.ma.is_masked(c) else float(c))
+    return np.array(out)
+
+
+@pytest.mark.parametrize("tight", [False, True])
+def test_fit_survey_chi_matches_oracle(tight):
+    """f1: fit_survey's per-sample chi (one batched launch) against the reference's
+    per-sample odeint + get_chi on the same LHS samples (seeded), at odeint's default
+    tolerances (measured max rel 9.5e-8) and at tight ones (2.8e-12)."""
+    kw = dict(rtol=1e-12, atol=1e-12) if tight else {}
+    m = product_model("two_i", **kw)
+    pn = m.get_pnames()
+    np.random.seed(11)
+    fs = m.fit_survey(samples=256)
+    assert list(fs.columns) == pn + ["chi"] and len(fs) == 256
+    assert np.array_equal(fs.index.to_numpy(), np.arange(256))
+    ref = _oracle_chi("two_i", fs[pn].to_numpy(dtype=float), tight=tight)
+    got = fs["chi"].to_numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    np.testing.assert_allclose(got, ref, rtol=1e-10 if tight else 1e-6)
+    # the batched survey is the batched integrate's chi, bit for bit
+    res = m.integrate_batch(fs[pn].to_numpy(), trajectory=False)
+    np.testing.assert_array_equal(res["chi"].cpu().numpy(), got)
+    # cpu_cores only reorders: the reference's round-robin workers, started last-first
+    np.random.seed(11)
+    fs3 = m.fit_survey(samples=256, cpu_cores=3)
+    assert np.array_equal(fs3["chi"].to_numpy(), np.concatenate([got[2::3], got[1::3], got[0::3]]))
+    assert list(fs3.index[:3]) == [0, 1, 2] and fs3.index[len(got[2::3])] == 0
+
+
+def test_mcmc_int_chain_starts_follow_the_cutchi_filter(monkeypatch):
+    """f1: MCMC(chain_inits=<int>) starts its chains from the survey samples whose chi
+    beats the shifted-data chi (Framework.py:993-1012): the same rows the reference's
+    filter keeps (oracle chi on the same seeded LHS samples; no sample within 1e-5 of
+    the threshold) and the same pandas ``sample`` draws from numpy's global RNG."""
+    from odelib_amd.Statistics import Samplers
     m = product_model("two_i")
-    np.random.seed(0)
-    fs = m.fit_survey(samples=512)
-    assert list(fs.columns) == m.get_pnames() + ["chi"]
-    assert len(fs) == 512 and np.isfinite(fs["chi"]).sum() > 100
-    res = m.integrate_batch(fs[m.get_pnames()].to_numpy(), trajectory=False)
-    np.testing.assert_array_equal(res["chi"].cpu().numpy(), fs["chi"].to_numpy())
-    eq = m.explore_equilibriums(samples=64)
-    assert list(eq.columns) == m.get_snames(after_summation=False) + m.get_pnames()
-    assert len(eq) == 64
+    pn = m.get_pnames()
+    n_chains, n_samples, sd = 8, 2000, 6.0
+    # the oracle's selection, replaying the same global-RNG consumption
+    np.random.seed(21)
+    ps = m._lhs_samples(n_samples)[pn].reset_index(drop=True)
+    chi = _oracle_chi("two_i", ps.to_numpy(dtype=float))
+    shifted = {s: np.exp(m._obs_logabundance[s] + sd * m._obs_logsigma[s]) for s in m._obs_logabundance}
+    cut = float(m.get_chi(shifted))
+    assert np.nanmin(np.abs(chi - cut)) / cut > 1e-5
+    ps["chi"] = chi
+    good = ps.dropna()
+    good = good[good["chi"] < cut]
+    assert len(good) >= 20
+    want = good.sample(n_chains, replace=True)[pn].to_numpy(dtype=float)
+    seen = {}
+
+    def capture(chains, **kw):
+        seen["theta"] = np.array([[float(np.asarray(c.parameters[p].val)) for p in pn] for c in chains])
+        seen["seeds"] = [c.random_seed for c in chains]
+        return pd.DataFrame({"chi": [0.0]})
+    monkeypatch.setattr(Samplers, "batched_metropolis_hastings", capture)
+    np.random.seed(21)
+    m.MCMC(chain_inits=n_chains, iterations_per_chain=10, fitsurvey_samples=n_samples, sd_fitdistance=sd,
+           print_report=False)
+    np.testing.assert_array_equal(seen["theta"], want)
+    assert seen["seeds"] == list(range(n_chains))
+
+
+@pytest.mark.parametrize("name", ["one_i", "two_i"])
+def test_explore_equilibriums_final_rows_match_odeint(name, capsys):
+    """f3: explore_equilibriums' final states (one batched launch) against the reference's
+    _Equilibrium_worker rows (odeint's last row per LHS sample, Framework.py:24-38):
+    within rtol = atol = 1e-6 of odeint at its default tolerances (measured 0.42 of that
+    budget) and of tight odeint (0.01)."""
+    m = product_model(name)
+    pn, sn = m.get_pnames(), m.get_snames(after_summation=False)
+    np.random.seed(5)
+    eq = m.explore_equilibriums(samples=128)
+    assert capsys.readouterr().out.startswith("Sampling with a Latin Hypercube scheme")
+    assert list(eq.columns) == sn + pn and len(eq) == 128
+    rows = eq[pn].to_numpy(dtype=float)
+    y0 = np.asarray(m.get_inits(), float)
+    for w in range(len(eq)):
+        for tol in ({}, dict(rtol=1e-13, atol=1e-13)):
+            final = cpu_ref.odeint_traj(RHS[name], y0, m.times, rows[w], **tol)[-1]
+            np.testing.assert_allclose(eq[sn].to_numpy()[w], final, rtol=1e-6, atol=1e-6, err_msg=f"{w} {tol}")
 
 
 # --------------------------------------------------------------------- C-ABI host pointers

@@ -439,3 +439,37 @@ def test_untranspilable_callable_is_bound_only_on_request():
     late = functools.partial(lambda y, t, ps, k: helper_style(y, t, ps) + (k if t > 4 else 0.0), k=1.0)
     with pytest.raises(ValueError):
         models.resolve(late, 4, 5, device_model="two_i", times=np.linspace(0, 6, 100))
+
+
+def test_worker_order_matches_reference_packaging():
+    """fit_survey / explore_equilibriums return rows in the order and with the index the
+    reference's cpu_cores workers produce (round-robin packaging, Framework.py:787-798;
+    jobs popped last-first and concatenated, :800-816)."""
+    from odelib_amd.Framework import _worker_order
+    for n, cores in [(10, 1), (10, 3), (7, 4), (3, 5), (0, 2)]:
+        worklist = [list() for _ in range(cores)]
+        for i in range(n):
+            worklist[i % cores].append(i)
+        order, index = [], []
+        while worklist:
+            rows = worklist.pop()
+            order += rows
+            index += range(len(rows))
+        o, ix = _worker_order(n, cores)
+        assert list(o) == order and list(ix) == index
+
+
+def test_sample_lhs_maps_the_hypercube_through_each_prior():
+    """Samplers.sample_lhs: one hypercube column per scalar parameter, in dict order,
+    through the prior's ppf (Samplers.py:6-51)."""
+    import scipy.stats
+    from odelib_amd import parameter
+    pars = {"a": parameter(stats_gen=scipy.stats.lognorm, hyperparameters={"s": 1, "scale": 2.0}, init_value=1.0),
+            "b": parameter(stats_gen=scipy.stats.norm, hyperparameters={"loc": 5, "scale": 0.1}, init_value=5.0)}
+    np.random.seed(4)
+    df = Samplers.sample_lhs(pars, samples=40)
+    np.random.seed(4)
+    u = Samplers.lhs_classic(2, 40)
+    assert list(df.columns) == ["a", "b"]
+    np.testing.assert_array_equal(df["a"].to_numpy(), scipy.stats.lognorm.ppf(u[:, 0], s=1, scale=2.0))
+    np.testing.assert_array_equal(df["b"].to_numpy(), scipy.stats.norm.ppf(u[:, 1], loc=5, scale=0.1))
