@@ -85,7 +85,8 @@ enum {
   OE_STATUS_NONFINITE = 1, /* a state became NaN/inf */
   OE_STATUS_NEGATIVE = 2,  /* a state went negative at an output time */
   OE_STATUS_MAXSTEP = 4,   /* step budget / step underflow: walker abandoned (NaN output) */
-  OE_STATUS_STIFF = 8      /* OE_METHOD_AUTO: the walker was integrated by the stiff method */
+  OE_STATUS_STIFF = 8,     /* OE_METHOD_AUTO: the walker was integrated by the stiff method */
+  OE_STATUS_INTERNAL = 16  /* oe_mh_run: an internal integrity check failed; the chain stopped storing */
 };
 
 /* call flags */

@@ -648,6 +648,10 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   m.theta = a->theta;
   m.y0 = a->y0;
   m.samples = a->samples;
+  m.n_rows = kept;
+  // self-test hook of the debug library's integrity checks (OE_MH_CHECKS): a row bound one
+  // short makes the last kept iteration fail the check; the product kernels never read it
+  if (getenv("OE_MH_CHECK_SELFTEST")) m.n_rows = kept - 1;
   m.status = a->status;
   // chain state: caller's final_stats buffer if given, else scratch
   if (a->final_stats) {

@@ -109,8 +109,8 @@ struct DevGuard {
 extern "C" {
 
 int oe_comm_unique_id(uint8_t* id, int32_t id_bytes) {
-  Rccl& R = rccl();
   if (!id || id_bytes != OE_COMM_ID_BYTES) return comm_fail(nullptr, OE_ERR_ARG, "oe_comm_unique_id: need a 128-byte buffer");
+  Rccl& R = rccl();
   if (!R.err.empty()) return comm_fail(nullptr, OE_ERR_UNSUPPORTED, R.err);
   ncclUniqueId u;
   OE_NCCL(nullptr, R.get_unique_id(&u));

@@ -55,7 +55,7 @@ struct DevProblem {
   double sstot;         // R² denominator
 };
 
-enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8 };
+enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8, ST_INTERNAL = 16 };
 
 // integrators (OE_METHOD_*): fixed-step RK4, DOPRI5, DOPRI5 with stiffness detection and
 // the Rosenbrock fallback for stiff / over-budget walkers (LSODA-like), Rosenbrock only
@@ -1139,7 +1139,16 @@ struct MHArgs {
   double* samples;         // [kept][P+5][W]
   double* cur;             // [4][W]: chi, rsquared, aic, n_accepted
   int32_t* status;         // [W]
+  int32_t n_rows;          // rows of samples (the kept iterations of this call)
 };
+
+// Integrity checks of the MH kernel's uniform state (below): compiled into the debug
+// library (make debug -> libodelib_amd_debug.so), whose MH parity run is a GPU test.
+// Off in the product library: even these few scalar compares move the register
+// allocation of the chain20 DOPRI5 MH kernel (scratch 176 -> 240 B/lane).
+#ifndef OE_MH_CHECKS
+#define OE_MH_CHECKS 0
+#endif
 
 // Element w of a walker-minor row [W] through a buffer resource: row base and size in
 // SGPRs, the lane's byte offset w*8 in one VGPR.  With plain pointers the compiler
@@ -1245,6 +1254,25 @@ __global__ void __launch_bounds__(256)
     theta = opaque(theta);
     y0g = opaque(y0g);
     cur = opaque(cur);
+#if OE_MH_CHECKS
+    // Integrity of the wave-uniform state every store below depends on:
+    // the row pointers carried through the integration (live in SGPRs or spilled across
+    // ~1000 steps) still equal the kernel arguments, the sample row lies inside the
+    // buffer, linked initial states name a parameter.  Lane offsets are in range by
+    // construction and range-checked by the buffer descriptors.  On a violation nothing
+    // more is stored and the walker's status carries ST_INTERNAL (a recorded assert: a
+    // device trap would take the process — and on this pool possibly the box — down).
+    {
+      bool sound = theta == ma.theta && y0g == ma.y0 && cur == ma.cur &&
+                   (it <= ma.burnin || (it - ma.row0 >= 0 && it - ma.row0 < ma.n_rows));
+#pragma unroll
+      for (int s = 0; s < S; ++s) sound = sound && ma.init_param[s] < P;
+      if (!sound) {
+        if (active && ma.status) ma.status[w] = ST_INTERNAL;
+        return;
+      }
+    }
+#endif
     const double u = Row(opaque(ma.u + (int64_t)(it - ma.draw_it0) * W), W).ld(off);
     double chi = Row(cur, W).ld(off), rsq = Row(cur + W, W).ld(off), aic = Row(cur + 2 * W, W).ld(off);
     double nacc = Row(cur + 3 * W, W).ld(off);
