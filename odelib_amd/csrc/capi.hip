@@ -529,6 +529,17 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   if (piped) {
     const dim3 grid((unsigned)((W + kPipeWalkers - 1) / kPipeWalkers)), block(256 + 64 * (2 << pipe_v));
     e->rk4_piped[pipe_v][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
+  } else if (c->method == OE_METHOD_DOPRI5 && !e->rtc && e->split_lanes > 0 && !(flags & OE_NO_SPLIT)) {
+    // wide chain models: one walker over K adjacent lanes (split.cuh), blocks of 256/K
+    // walkers dealt to the XCDs in runs of 512 walkers as the one-lane kernel's
+    const int K = e->split_lanes;
+    const int64_t per_block = kBlock / K;
+    const dim3 grid((unsigned)((W + per_block - 1) / per_block)), block(kBlock);
+    ia.half = 0;
+    ia.xcd_remap = (flags & OE_NO_XCD_REMAP) ? 0
+                   : (flags & OE_XCD_RANGES) ? (int32_t)std::max<int64_t>(1, (int64_t)grid.x / 8)
+                                             : (int32_t)std::max<int64_t>(1, 512 / per_block);
+    e->dopri5_split[ia.traj ? 1 : 0][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
   } else {
     // RK4 trajectories of 5+ states at <= 1 wave per SIMD are store-issue bound: run
     // 32 walkers per wave (twice the storing waves; same bits).  Measured on MI355X at

@@ -22,6 +22,8 @@ struct Entry {
   IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > 8
   MHLaunch mh[4];
   StiffWaveLaunch stiff_wave[2][2];  // [traj][nt]: S > kStiffRegS stiff redo, one wave per walker
+  IntegrateLaunch dopri5_split[2][2];  // [traj][nt]: DOPRI5 with split_lanes lanes per walker (split.cuh)
+  int32_t split_lanes = 0;             // 0: the model has no split kernel
   const RtcModule* rtc = nullptr;  // user RHS compiled at run time (launchers above unused)
 };
 
@@ -77,6 +79,16 @@ inline hipError_t launch_stiff_wave_entry(const Entry* e, int traj, int nt, cons
   return hipGetLastError();
 }
 
+template <int N, int K, bool TRAJ, bool NT>
+void launch_split(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_integrate_split<N, K, TRAJ, NT>), g, b, 0, s, pb, ia);
+}
+// lanes per walker of a model's split DOPRI5 kernel (split.cuh): the built-in chain only
+template <class M>
+struct SplitOf { static constexpr int K = 0; };
+template <int N>
+struct SplitOf<Chain<N>> { static constexpr int K = split_lanes_chain<N>(); };
+
 template <class M, int METHOD>
 void fill_method(Entry& e) {
   e.integrate[METHOD][0][0] = launch_integrate<M, METHOD, false, false>;
@@ -103,6 +115,14 @@ Entry make_entry(int32_t model_id) {
     e.stiff_wave[0][1] = launch_stiff_wave<M, false, false>;
     e.stiff_wave[1][0] = launch_stiff_wave<M, true, false>;
     e.stiff_wave[1][1] = launch_stiff_wave<M, true, true>;
+  }
+  if constexpr (SplitOf<M>::K > 0) {
+    constexpr int K = SplitOf<M>::K;
+    e.split_lanes = K;
+    e.dopri5_split[0][0] = launch_split<M::S, K, false, false>;
+    e.dopri5_split[0][1] = launch_split<M::S, K, false, false>;
+    e.dopri5_split[1][0] = launch_split<M::S, K, true, false>;
+    e.dopri5_split[1][1] = launch_split<M::S, K, true, true>;
   }
   if constexpr (M::S <= 8) {
     e.rk4_piped[0][0] = launch_rk4_piped<M, false, 2>;

@@ -1322,3 +1322,4 @@ __global__ void __launch_bounds__(256)
 
 }  // namespace oe
 #include "stiff_wave.cuh"
+#include "split.cuh"

@@ -247,7 +247,7 @@ class Engine:
     # -- batched integrate -------------------------------------------------------------------
     def integrate(self, y0, theta, trajectory: bool = True, traj_out=None, nt_stores: bool = True,
                   sync: bool = True, pipelined=None, half_waves: bool = False,
-                  xcd_remap=True, timing: bool = True):
+                  xcd_remap=True, timing: bool = True, split: bool = True):
         """y0 [S][W], theta [P][W] → dict(traj [T][S][W] | None, chi [W], ssres [W], status [W]).
 
         ``pipelined=True`` (or 2, 4, 8: store waves per 4 compute waves) selects the
@@ -256,7 +256,9 @@ class Engine:
         ``xcd_remap=False`` keeps blockIdx-order walker blocks instead of runs of 512
         walkers dealt to the XCDs in turn; ``xcd_remap="ranges"`` gives each XCD one
         contiguous walker range (same results either way).  ``timing=False`` records no library events
-        around the launch (``last_kernel_ms`` is then unavailable for this call)."""
+        around the launch (``last_kernel_ms`` is then unavailable for this call).
+        ``split=False`` keeps one lane per walker in DOPRI5 for the models whose kernel
+        otherwise spreads a walker over 2 or 4 lanes (OE_NO_SPLIT; the wide built-in chain)."""
         torch = self.torch
         pb = self.problem
         theta_t = theta if isinstance(theta, torch.Tensor) else np.asarray(theta)
@@ -277,7 +279,7 @@ class Engine:
         flags = N.OE_ASYNC | (N.OE_NT_STORES if nt_stores else 0) | pipe \
             | (N.OE_HALF_WAVES if half_waves else 0) \
             | (N.OE_XCD_RANGES if xcd_remap == "ranges" else 0 if xcd_remap else N.OE_NO_XCD_REMAP) \
-            | (0 if timing else N.OE_NO_TIMING)
+            | (0 if timing else N.OE_NO_TIMING) | (0 if split else N.OE_NO_SPLIT)
         self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)
         if sync:
             torch.cuda.synchronize(self.dev)

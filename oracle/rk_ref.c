@@ -11,7 +11,8 @@
  *     (compiled with -ffp-contract=off: bitwise equal to the kernel);
  *   - DOPRI5 with the wavefront rule: walkers 64g..64g+63 share one step size,
  *     the step error is the max over those lanes of the per-lane max norm
- *     (DESIGN.md §3.2); equal to the kernel up to libm-vs-ocml pow() ulps;
+ *     (DESIGN.md §3.2); for the split kernel (split.cuh, K lanes per walker) groups of
+ *     64/K walkers, each walker's norm reduced over its lanes' states in a lane tree;
  *   - the fused likelihood: chi = Σ finite (O − log C)²/(2S²) (stats.py:41),
  *     ssres = Σ non-NaN (C − exp O)² (stats.py:52);
  *   - the batched Metropolis–Hastings step (Samplers.py:104-153) with replay or
@@ -48,6 +49,9 @@ typedef struct {
   double rtol, atol;
   int wave_redo; /* batched integrate of S > 8: stiff walkers redone one per group
                     (odelib_amd/csrc/stiff_wave.cuh: one wave per walker, own step size) */
+  int split;     /* DOPRI5 with a walker over `split` lanes (odelib_amd/csrc/split.cuh): groups of
+                    64/split walkers share a step size; a walker's error norm is the argmax over
+                    each lane's states, combined in a tree of lanes (lower lane kept on ties) */
 } Prob;
 
 static void rhs(const Prob* pb, const double* y, double t, const double* ps, double* dy) {
@@ -291,16 +295,28 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
       for (int s = 0; s < S; ++s)
         q->yn[s] = fma(b76, q->k6[s], fma(b75, q->k5[s], fma(b74, q->k4[s], fma(b73, q->k3[s], fma(b71, q->k1[s], q->y[s])))));
       rhs(pb, q->yn, t + h, pl, q->k7);
-      /* argmax of |e|/sk by exact cross-multiplication, then one division */
-      double num = 0.0, den = 1.0, nfe = 0.0;
-      for (int s = 0; s < S; ++s) {
-        double e = fma(g7, q->k7[s], fma(g6, q->k6[s], fma(g5, q->k5[s], fma(g4, q->k4[s], fma(g3, q->k3[s], g1 * q->k1[s])))));
-        double ae = fabs(e);
-        double sk = fma(rtol, fmax(fabs(q->y[s]), fabs(q->yn[s])), atol);
-        nfe = fma(ae, 0.0, nfe);
-        if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
+      /* argmax of |e|/sk by exact cross-multiplication, then one division; a split walker
+         takes the argmax per lane (states [r*m, r*m+m)), then the lane tree */
+      const int K = pb->split > 1 ? pb->split : 1, m = S / K;
+      double pnum[4], pden[4], nfe = 0.0;
+      for (int r = 0; r < K; ++r) {
+        double num = 0.0, den = 1.0, nfr = 0.0;
+        for (int j = 0; j < m; ++j) {
+          const int s = r * m + j;
+          double e = fma(g7, q->k7[s], fma(g6, q->k6[s], fma(g5, q->k5[s], fma(g4, q->k4[s], fma(g3, q->k3[s], g1 * q->k1[s])))));
+          double ae = fabs(e);
+          double sk = fma(rtol, fmax(fabs(q->y[s]), fabs(q->yn[s])), atol);
+          nfr = fma(ae, 0.0, nfr);
+          if (j == 0 || ae * den > num * sk) { num = ae; den = sk; }
+        }
+        pnum[r] = num;
+        pden[r] = den;
+        nfe = nfe + nfr;
       }
-      double el = num / den;
+      for (int d = 1; d < K; d <<= 1)
+        for (int r = 0; r < K; r += 2 * d) /* lanes r (lower) and r + d (upper) */
+          if (pnum[r + d] * pden[r] > pnum[r] * pden[r + d]) { pnum[r] = pnum[r + d]; pden[r] = pden[r + d]; }
+      double el = pnum[0] / pden[0];
       if (!isfinite(el) || isnan(nfe)) el = 1e30;
       if (q->dead) el = 0.0;
       q->el = el;
@@ -787,13 +803,17 @@ static Prob make_prob(int model, int S, int P, int T, const double* times, int n
 }
 
 /* Integrate walkers [g*64, g*64+64) of a batch; y0/theta/outputs are [..][W]. */
+/* walkers per lockstep group: 64, or 64/split for the split DOPRI5 kernel */
+static int group_size(const Prob* pb) { return pb->split > 1 ? LANES / pb->split : LANES; }
+
 static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* y0, const double* theta,
                             double* traj, Acc* out_acc /*[64]*/) {
   static __thread Lane L[LANES];
   static __thread double p[LANES * MAXP];
   const int S = pb->S, P = pb->P;
-  for (int l = 0; l < LANES; ++l) {
-    int64_t gw = g * LANES + l;
+  const int G = group_size(pb);
+  for (int l = 0; l < G; ++l) {
+    int64_t gw = g * G + l;
     int active = gw < W;
     int64_t w = active ? gw : W - 1;
     L[l].active = active;
@@ -818,7 +838,7 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
     for (int l = 0; l < LANES; ++l)
       if (L[l].active) check_finite(pb->S, L[l].y, &L[l].a);
   } else if (pb->method == METHOD_DOPRI5) {
-    dopri5_group(pb, L, LANES, p, traj, W, 0);
+    dopri5_group(pb, L, G, p, traj, W, 0);
   } else if (pb->method == METHOD_AUTO) {
     auto_group(pb, L, LANES, p, traj, W);
   } else {
@@ -830,24 +850,27 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
       rodas_group(pb, L, LANES, p, traj, W);
     }
   }
-  for (int l = 0; l < LANES; ++l) out_acc[l] = L[l].a;
+  for (int l = 0; l < G; ++l) out_acc[l] = L[l].a;
 }
 
 int ref_integrate(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                   const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                   int substeps, double rtol, double atol, int max_steps, int64_t W, const double* y0,
-                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status) {
+                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status, int split) {
   if (S > MAXS || P > MAXP || W <= 0) return -1;
+  if (split > 1 && (method != METHOD_DOPRI5 || split > 4 || S % split)) return -1;
   Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
   pb.wave_redo = S > 8; /* ode_kernels.cuh kStiffRegS */
-  const int64_t ngroups = (W + LANES - 1) / LANES;
+  pb.split = split;
+  const int G = group_size(&pb);
+  const int64_t ngroups = (W + G - 1) / G;
   /* groups are independent: OpenMP over groups gives the same bits as the serial loop */
 #pragma omp parallel for schedule(dynamic, 4)
   for (int64_t g = 0; g < ngroups; ++g) {
     Acc acc[LANES];
     integrate_group(&pb, W, g, y0, theta, traj, acc);
-    for (int l = 0; l < LANES; ++l) {
-      int64_t w = g * LANES + l;
+    for (int l = 0; l < G; ++l) {
+      int64_t w = g * G + l;
       if (w >= W) break;
       if (chi) chi[w] = acc[l].nvalid ? acc[l].chi : NAN;
       if (ssres) ssres[w] = acc[l].ssres;

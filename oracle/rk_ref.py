@@ -28,7 +28,7 @@ def lib():
         vp, i32, i64, d, u64 = C.c_void_p, C.c_int, C.c_int64, C.c_double, C.c_uint64
         L.ref_integrate.restype = C.c_int
         L.ref_integrate.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, d, d, i32,
-                                    i64, vp, vp, vp, vp, vp, vp]
+                                    i64, vp, vp, vp, vp, vp, vp, i32]
         L.ref_mh.restype = C.c_int
         L.ref_mh.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, d, d, i32, d, i32,
                              i64, i64, i32, i32, i32, u64, d, vp, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -77,8 +77,26 @@ class Problem:
                 self.rtol, self.atol, self.max_steps)
 
 
-def integrate(fp, y0, theta, trajectory=True):
+def product_split(fp) -> int:
+    """Lanes per walker of the product's DOPRI5 integrate for this problem (the rule in
+    include/odelib_amd.h, OE_NO_SPLIT): the built-in chain with 14..22 states (even) runs
+    2 lanes per walker, 24+ states (a multiple of 4) 4 lanes; everything else 1."""
+    S = int(fp.n_states)
+    if int(fp.model_id) != 3 or fp.method != "dopri5" or getattr(fp, "custom_source", None) is not None:
+        return 1
+    if 14 <= S <= 22 and S % 2 == 0:
+        return 2
+    if S >= 24 and S % 4 == 0:
+        return 4
+    return 1
+
+
+def integrate(fp, y0, theta, trajectory=True, split=None):
+    """The engine's integrate restated.  ``split``: lanes per walker of the DOPRI5 kernel
+    being checked (None: the product's choice for this problem, ``product_split``; 1: the
+    one-lane grouping, as the product's OE_NO_SPLIT)."""
     pr = Problem(fp)
+    split = product_split(fp) if split is None else int(split)
     y0 = np.ascontiguousarray(y0, dtype=np.float64)
     theta = np.ascontiguousarray(theta, dtype=np.float64)
     W = theta.shape[1]
@@ -86,7 +104,8 @@ def integrate(fp, y0, theta, trajectory=True):
     chi = np.empty(W)
     ssres = np.empty(W)
     status = np.empty(W, np.int32)
-    rc = lib().ref_integrate(*pr.args(), W, _p(y0), _p(theta), _p(traj), _p(chi), _p(ssres), _p(status))
+    rc = lib().ref_integrate(*pr.args(), W, _p(y0), _p(theta), _p(traj), _p(chi), _p(ssres), _p(status),
+                             split if split > 1 else 0)
     if rc:
         raise RuntimeError("ref_integrate failed")
     return {"traj": traj, "chi": chi, "ssres": ssres, "status": status}

@@ -13,7 +13,7 @@
 int ref_integrate(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                   const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                   int substeps, double rtol, double atol, int max_steps, int64_t W, const double* y0,
-                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status);
+                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status, int split);
 int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx, const uint64_t* mask,
            const double* O, const double* two_s2, const double* lin, int method, int substeps, double rtol,
            double atol, int max_steps, double sstot, int pnum, int64_t W, int64_t walker_offset, int nits, int burnin,
@@ -33,7 +33,7 @@ static double times[T];
 static int32_t tidx[NOBS] = {0, 8, 15, 15, 30, 44, 52, 59};
 static double O[NOBS], two_s2[NOBS], lin[NOBS];
 
-static void run_case(int model, int S, int P, int64_t W, int method, int with_traj) {
+static void run_case(int model, int S, int P, int64_t W, int method, int with_traj, int split) {
   const double base[6] = {7.475e-9, 1.069e-7, 19.73, 1.934, 2.799, 10981000.0};
   uint64_t mask[NOBS];
   for (int k = 0; k < NOBS; ++k) mask[k] = (k % 2) ? (1ull << (S - 1)) : ((1ull << (S - 1)) - 1ull);
@@ -55,7 +55,7 @@ static void run_case(int model, int S, int P, int64_t W, int method, int with_tr
   double* ss = malloc(sizeof(double) * W);
   int32_t* st = malloc(sizeof(int32_t) * W);
   int rc = ref_integrate(model, S, P, T, times, NOBS, tidx, mask, O, two_s2, lin, method, 2, 1.49012e-8, 1.49012e-8,
-                         60, W, y0, th, traj, chi, ss, st);
+                         60, W, y0, th, traj, chi, ss, st, split);
   if (rc) { fprintf(stderr, "ref_integrate rc=%d (model %d S %d method %d)\n", rc, model, S, method); exit(1); }
   /* Metropolis-Hastings: Philox, then replay with a linked initial state (P + 1) */
   const int nits = 9, burnin = 3, kept = nits - 1 - burnin;
@@ -99,12 +99,14 @@ int main(void) {
     lin[k] = exp(O[k]);
   }
   for (int method = 0; method < 4; ++method) {
-    run_case(2, 4, 5, method == 3 ? 12 : 70, method, 1);  /* two_i: ragged groups (Rosenbrock: one) */
-    run_case(2, 4, 5, 3, method, 0);     /* one partial group, chi only */
+    run_case(2, 4, 5, method == 3 ? 12 : 70, method, 1, 0);  /* two_i: ragged groups (Rosenbrock: one) */
+    run_case(2, 4, 5, 3, method, 0, 0);     /* one partial group, chi only */
   }
-  run_case(3, 20, 5, 66, 1, 1);          /* chain20 DOPRI5 */
-  run_case(3, 20, 5, 66, 2, 1);          /* chain20 auto: the wide (one walker per group) redo */
-  run_case(3, 10, 5, 12, 3, 0);          /* chain10 Rosenbrock, private-memory matrices */
+  run_case(3, 20, 5, 66, 1, 1, 0);          /* chain20 DOPRI5 */
+  run_case(3, 20, 5, 66, 1, 1, 2);          /* chain20 DOPRI5, split over 2 lanes (32-walker groups) */
+  run_case(3, 32, 5, 40, 1, 0, 4);          /* chain32 DOPRI5, split over 4 lanes */
+  run_case(3, 20, 5, 66, 2, 1, 0);          /* chain20 auto: the wide (one walker per group) redo */
+  run_case(3, 10, 5, 12, 3, 0, 0);          /* chain10 Rosenbrock, private-memory matrices */
   puts("SANITIZE OK");
   return 0;
 }

@@ -149,6 +149,46 @@ def test_dopri5_vs_c_restatement(spec, W):
     assert np.array_equal(lean["status"] & 5, out["status"] & 5)
 
 
+@pytest.mark.parametrize("spec", ["chain10", "chain16", "chain20", "chain24", "chain32"])
+@pytest.mark.parametrize("W", [1, 33, 200])
+def test_split_dopri5_bitwise_vs_c_restatement(spec, W):
+    """The split DOPRI5 kernel (a walker over 2 lanes for chain16/20, 4 for chain24/32;
+    chain10 stays one lane per walker; split.cuh): bitwise
+    against the C restatement of the same grouping (64/K walkers per step size, the lane
+    tree of the error norm), chi-only launch equal to the trajectory one; and with
+    OE_NO_SPLIT the one-lane kernel, bitwise against the 64-walker grouping."""
+    m = _model(spec, "dopri5")
+    fp = m.fit_problem()
+    assert rk_ref.product_split(fp) == {"chain10": 1, "chain16": 2, "chain20": 2, "chain24": 4, "chain32": 4}[spec]
+    theta = _walkers(spec, W, seed=7)
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(fp, y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"])
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
+    assert np.array_equal(out["status"], ref["status"])
+    _, lean = _run(m, theta, y0=y0, trajectory=False)
+    for key in ("chi", "ssres"):
+        assert np.array_equal(lean[key], out[key], equal_nan=True), key
+    one = m.engine().integrate(y0, theta, split=False)
+    ref1 = rk_ref.integrate(fp, y0, theta, split=1)
+    assert np.array_equal(one["traj"].cpu().numpy(), ref1["traj"])
+    # both groupings meet the tolerance: same solution to well within rtol
+    np.testing.assert_allclose(out["traj"], ref1["traj"], rtol=1e-6, atol=1e-4)
+
+
+def test_split_dopri5_evicts_a_pinning_walker():
+    """A walker that cannot finish within max_steps is evicted in the split kernel too
+    (status MAXSTEP on both of its lanes' outputs, NaN rows), bitwise as the C oracle."""
+    m = _model("chain20", "dopri5", max_steps=150)
+    theta = _walkers("chain20", 70, seed=5)
+    theta[4, 3] = 1e9
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert out["status"][3] & N.OE_STATUS_MAXSTEP and np.isnan(out["traj"][-1, :, 3]).all()
+    assert np.array_equal(out["traj"], ref["traj"], equal_nan=True)
+    assert np.array_equal(out["status"], ref["status"])
+
+
 # --------------------------------------------------------------------- reference algorithm
 @pytest.mark.parametrize("spec,method,substeps,atol", [
     ("zero_i", "rk4", 4, 1e-6), ("one_i", "rk4", 1, 1e-6), ("two_i", "rk4", 1, 1e-6),
