@@ -507,8 +507,11 @@ def extra_configs(args, R, T, P):
             ("C2-stiffmix-auto", "two_i", "auto", 65536, 1e-3, 1, "rtol=atol=1.49012e-8"),
             ("C3", "chain20", "rk4", 262144, 0.0, 1, "vs tight odeint: rtol 1e-6, atol 1e-4 (test-pinned)"),
             ("C3-rk4x3", "chain20", "rk4", 262144, 0.0, 3, "vs tight odeint: rtol 1e-6, atol 1e-6 (test-pinned)"),
-            ("C3-dopri5", "chain20", "dopri5", 262144, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"))
+            ("C3-dopri5", "chain20", "dopri5", 262144, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"),
+            # the same with one lane per walker (OE_NO_SPLIT): the round-2 kernel, for reference
+            ("C3-dopri5-onelane", "chain20", "dopri5", 262144, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"))
     for name, model, method, W, stiff, subs, tol in cfgs:
+        split = not name.endswith("-onelane")
         ex, y0x = R.engine(model, method, T, subs)
         Sx = len(y0x)
         thh = synthetic_walkers(W, P)
@@ -524,13 +527,13 @@ def extra_configs(args, R, T, P):
         # without event markers, timed by two events on the stream
         K = 20 if not n_stiff else 3
         warm(lambda: ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False,
-                                  xcd_remap=XCD_ARG[args.xcd]))
+                                  xcd_remap=XCD_ARG[args.xcd], split=split))
         sx = torch.cuda.current_stream(R.dev)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record(sx)
         for _ in range(K):
             outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False,
-                                xcd_remap=XCD_ARG[args.xcd])
+                                xcd_remap=XCD_ARG[args.xcd], split=split)
         ev[1].record(sx)
         torch.cuda.synchronize(R.dev)
         kms = ev[0].elapsed_time(ev[1]) / K
@@ -542,6 +545,8 @@ def extra_configs(args, R, T, P):
                        "hbm_frac": byt / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "tolerance": tol}
         if method == "rk4":
             extra[name]["rk4_substeps"] = subs
+        if model == "chain20" and method == "dopri5":
+            extra[name]["lanes_per_walker"] = 2 if split else 1
         if n_stiff:
             stx = outx["status"].cpu().numpy()
             extra[name]["walkers_flagged_stiff"] = int(((stx & 8) != 0).sum())

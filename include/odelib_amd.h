@@ -109,7 +109,7 @@ enum {
   OE_PIPE_8 = 1024u,
   OE_XCD_RANGES = 2048u, /* oe_integrate: one contiguous walker range per XCD instead (the r01
                            mapping; same results) */
-  OE_NO_SPLIT = 4096u   /* oe_integrate, OE_METHOD_DOPRI5: one lane per walker even for the models
+  OE_NO_SPLIT = 4096u   /* oe_integrate / oe_mh_run, OE_METHOD_DOPRI5: one lane per walker even for the models
                            whose DOPRI5 kernel splits a walker over K lanes (built-in chain with
                            14..22 states: K = 2; 24+ states, a multiple of 4: K = 4).  A split
                            wave holds 64/K walkers, which share one step size, so results differ

@@ -674,6 +674,18 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   }
 
   const dim3 grid((unsigned)((W + kBlock - 1) / kBlock)), block(kBlock);
+  // wide chain models, DOPRI5: the chain over K lanes (split.cuh); the kernel addresses its
+  // states in one [S][W] descriptor, so S*W*8 must stay below 4 GiB
+  const bool split = c->method == OE_METHOD_DOPRI5 && !e->rtc && e->mh_split && !(flags & OE_NO_SPLIT) &&
+                     (int64_t)S * W * 8 < (int64_t(1) << 32);
+  const dim3 mh_grid = split ? dim3((unsigned)((W * e->split_lanes + kBlock - 1) / kBlock)) : grid;
+  auto launch_mh = [&](const MHArgs& args) -> hipError_t {
+    if (split) {
+      e->mh_split(c->dp, args, mh_grid, block, c->stream);
+      return hipGetLastError();
+    }
+    return launch_mh_entry(e, c->method, c->dp, args, grid, block, c->stream);
+  };
   int chunk = a->chunk > 0 ? a->chunk : 25;
   const bool philox = a->rng_mode == OE_RNG_PHILOX, numpy = a->rng_mode == OE_RNG_NUMPY;
   DrawArgs d{};
@@ -729,7 +741,7 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
     m.init = 1;
     m.it0 = 0;
     m.it1 = 0;
-    OE_HIP(c, launch_mh_entry(e, c->method, c->dp, m, grid, block, c->stream));
+    OE_HIP(c, launch_mh(m));
   }
   m.init = 0;
   for (int it0 = it_start; it0 < a->nits; it0 += chunk) {
@@ -748,7 +760,7 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       hipLaunchKernelGGL(k_np_draws, grid, block, 0, c->stream, nd);
       OE_HIP(c, hipGetLastError());
     }
-    OE_HIP(c, launch_mh_entry(e, c->method, c->dp, m, grid, block, c->stream));
+    OE_HIP(c, launch_mh(m));
   }
   OE_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;

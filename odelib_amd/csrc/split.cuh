@@ -399,3 +399,147 @@ constexpr int split_lanes_chain() { return (N >= 14 && N <= 22 && N % 2 == 0) ? 
 #endif
 
 }  // namespace oe
+
+namespace oe {
+
+// Metropolis–Hastings (Samplers.py:104-153) for the split DOPRI5 models: the chain of
+// walker w lives on its K lanes.  The walker's chain state (θ, the current point) is read
+// and written by lane 0 only and broadcast to the other lanes with DPP, so no lane ever
+// reads a row another lane writes; every lane then holds the same proposal, integrates its
+// states, sees the same chi (the observation sums are group-wide) and takes the same
+// decision.  Each lane reads and writes its own linked '<state>0' initial states.
+// Otherwise k_mh's structure (chain state in HBM between iterations, buffer-descriptor
+// rows, opaque row pointers).
+template <int N, int K>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+    k_mh_split(const DevProblem pb, const MHArgs ma) {
+  constexpr int m = N / K;
+  constexpr int PMAX = 5 + 4;  // kPmax<Chain<N>>: the model's 5 plus up to 4 '<state>0' parameters
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = (int)(threadIdx.x & (K - 1));
+  const int64_t gw = gt / K;
+  const bool active = gw < ma.W;
+  const bool writer = active && r == 0;
+  const int64_t w = active ? gw : ma.W - 1;
+  const int64_t W = ma.W;
+  const int P = pb.P;
+  double* __restrict__ theta = ma.theta;
+  double* __restrict__ y0g = ma.y0;
+  const uint32_t off = (uint32_t)w * 8u;
+  const uint32_t off_s = (uint32_t)(w * 8 + (int64_t)r * m * W * 8);  // this lane's first state in [S][W]
+  const Row ys(y0g, (int64_t)N * W);
+  // lane 0's value of a walker row, on all K lanes
+  auto ld0 = [&](const double* row) { return dpp_f64<QuadCtl<K>::first>(Row(row, W).ld(off)); };
+  // the '<state>0' parameter of local state j (a select over the K lanes' global indices)
+  auto linked = [&](int j) {
+    int pi = ma.init_param[j];
+#pragma unroll
+    for (int q = 1; q < K; ++q) pi = (r == q) ? ma.init_param[q * m + j] : pi;
+    return pi;
+  };
+  bool any_linked = false;  // wave-uniform
+#pragma unroll
+  for (int s = 0; s < N; ++s) any_linked = any_linked || ma.init_param[s] >= 0;
+
+  if (ma.init) {  // a-priori fit (Samplers.py:88-91)
+    double th[PMAX], y[m];
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) th[j] = (j < P) ? ld0(theta + (int64_t)j * W) : 0.0;
+#pragma unroll
+    for (int j = 0; j < m; ++j) y[j] = ys.ld(off_s + (uint32_t)(j * W * 8));
+    Acc a = acc_init();
+    integrate_dopri5_split<N, K, false, false>(pb, y, th, nullptr, W, off_s, active, r, a);
+    if (writer) {
+      const double chi = a.nvalid ? a.chi : __builtin_nan("");
+      Row(ma.cur, W).st(off, chi);
+      Row(ma.cur + W, W).st(off, 1.0 - a.ssres / pb.sstot);
+      Row(ma.cur + 2 * W, W).st(off, -2.0 * (-chi) + 2.0 * (double)pb.pnum);
+      Row(ma.cur + 3 * W, W).st(off, 0.0);
+      if (ma.status) ma.status[w] = finish(a);
+    }
+    return;
+  }
+  double* __restrict__ cur = ma.cur;
+  const int PS = P + 5;
+  // the proposal θ' = exp(log θ + dz) for walking parameters (Framework.py:107-122),
+  // formed from lane 0's θ: identical values every time it is formed
+  auto propose = [&](int it, double (&tn)[PMAX]) {
+    const double* dz = opaque(ma.dz + (int64_t)(it - ma.draw_it0) * P * W);
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) {
+      const double thj = (j < P) ? ld0(theta + (int64_t)j * W) : 0.0;
+      tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? oe_exp(oe_log(thj) + Row(dz + (int64_t)j * W, W).ld(off)) : thj;
+    }
+  };
+  for (int it = ma.it0; it < ma.it1; ++it) {
+    double y[m], p5[5];
+    theta = opaque(theta);
+    y0g = opaque(y0g);
+    {
+      double tn[PMAX];
+      propose(it, tn);
+#pragma unroll
+      for (int j = 0; j < m; ++j) {
+        const int pi = linked(j);
+        y[j] = (ma.any_walk && pi >= 0) ? pick(tn, pi) : ys.ld(off_s + (uint32_t)(j * W * 8));
+      }
+#pragma unroll
+      for (int j = 0; j < 5; ++j) p5[j] = tn[j];  // the RHS reads the model's 5 parameters only
+    }
+    Acc a = acc_init();
+    integrate_dopri5_split<N, K, false, false>(pb, y, p5, nullptr, W, off_s, active, r, a);
+    const double chin = a.nvalid ? a.chi : __builtin_nan("");
+    theta = opaque(theta);
+    y0g = opaque(y0g);
+    cur = opaque(cur);
+    double tn[PMAX];  // the proposal again (not held in registers across the integration)
+    propose(it, tn);
+    const double u = Row(opaque(ma.u + (int64_t)(it - ma.draw_it0) * W), W).ld(off);
+    double chi = ld0(cur), rsq = ld0(cur + W), aic = ld0(cur + 2 * W);
+    double nacc = ld0(cur + 3 * W);
+    const double lr = oe_exp(chi - chin);
+    const double accp = oe_exp(oe_log(lr));
+    const bool acc = accp > u;
+    // the current parameters (lane 0's, on every lane), for the rejected proposal's
+    // linked states and the sample row
+    double told[PMAX];
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) told[j] = (j < P) ? ld0(theta + (int64_t)j * W) : 0.0;
+    if (acc) {
+      chi = chin;
+      rsq = 1.0 - a.ssres / pb.sstot;
+      aic = -2.0 * (-chi) + 2.0 * (double)pb.pnum;
+      nacc += 1.0;
+      if (writer) {
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j)
+          if (j < P) Row(theta + (int64_t)j * W, W).st(off, tn[j]);
+        Row(cur, W).st(off, chi);
+        Row(cur + W, W).st(off, rsq);
+        Row(cur + 2 * W, W).st(off, aic);
+        Row(cur + 3 * W, W).st(off, nacc);
+        if (ma.status) ma.status[w] = finish(a);
+      }
+    }
+    if (ma.any_walk && any_linked && active) {
+#pragma unroll
+      for (int j = 0; j < m; ++j) {
+        const int pi = linked(j);
+        if (pi >= 0) ys.st(off_s + (uint32_t)(j * W * 8), acc ? pick(tn, pi) : pick(told, pi));
+      }
+    }
+    if (it > ma.burnin && writer) {
+      double* row = ma.samples + (int64_t)(it - ma.row0) * PS * W;
+#pragma unroll
+      for (int j = 0; j < PMAX; ++j)
+        if (j < P) Row(row + (int64_t)j * W, W).st(off, acc ? tn[j] : told[j]);
+      Row(row + (int64_t)P * W, W).st(off, chi);
+      Row(row + (int64_t)(P + 1) * W, W).st(off, rsq);
+      Row(row + (int64_t)(P + 2) * W, W).st(off, aic);
+      Row(row + (int64_t)(P + 3) * W, W).st(off, (double)it);
+      Row(row + (int64_t)(P + 4) * W, W).st(off, nacc / (double)it);
+    }
+  }
+}
+
+}  // namespace oe

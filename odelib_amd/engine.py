@@ -310,7 +310,7 @@ class Engine:
     def mh_run(self, theta, y0, nits: int, burnin: int, walk_mask, init_param=None, rng: str = "philox",
                seed: int = 0, replay=None, step_sd: float = 0.05, walker_offset: int = 0, chunk: int = 0,
                sync: bool = True, numpy_seeds=None, prior_draws: int = 0, resume=None,
-               allow_unverified: bool = False):
+               allow_unverified: bool = False, split: bool = True):
         """Run W chains; returns dict(samples [kept][P+5][W], theta, y0, final [4][W], status).
 
         rng='replay' takes ``replay=(dz [nits-1][P][W], u [nits-1][W])`` (e.g. from
@@ -324,7 +324,9 @@ class Engine:
         are the chain state after iteration ``resume['next_it'] - 1``; iterations
         next_it..nits-1 run with the same draws as one uninterrupted run, and samples
         holds the kept rows from max(next_it, burnin+1) on.  ``allow_unverified`` resumes a
-        checkpoint that predates the random-stream record (see ``check_resume``)."""
+        checkpoint that predates the random-stream record (see ``check_resume``).
+        ``split=False``: one lane per chain for the models whose DOPRI5 MH kernel otherwise
+        spreads a chain over 2 or 4 lanes (OE_NO_SPLIT)."""
         torch = self.torch
         pb = self.problem
         P, S = pb.n_params, pb.n_states
@@ -396,7 +398,7 @@ class Engine:
         a.final_stats = final.data_ptr()
         a.status = status.data_ptr()
         self._sync_stream()
-        self.ctx.mh_run(a, N.OE_ASYNC)
+        self.ctx.mh_run(a, N.OE_ASYNC | (0 if split else N.OE_NO_SPLIT))
         if sync:
             torch.cuda.synchronize(self.dev)
         out = {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status,

@@ -927,9 +927,12 @@ int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const
            double atol, int max_steps, double sstot, int pnum, int64_t W, int64_t walker_offset, int nits, int burnin,
            int rng_mode, uint64_t seed, double step_sd, const uint8_t* walk, const int32_t* init_param,
            const double* dz, const double* uu, double* theta /*[P][W] io*/, double* y0 /*[S][W] io*/,
-           double* samples /*[kept][P+5][W]*/, double* final_stats /*[4][W]*/, int32_t* status /*[W]*/) {
+           double* samples /*[kept][P+5][W]*/, double* final_stats /*[4][W]*/, int32_t* status /*[W]*/, int split) {
   if (S > MAXS || P > MAXP || W <= 0) return -1;
+  if (split > 1 && (method != METHOD_DOPRI5 || split > 4 || S % split)) return -1;
   Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
+  pb.split = split; /* the split MH kernel (split.cuh k_mh_split): 64/split walkers per step size */
+  const int G = group_size(&pb);
   int any_walk = 0;
   for (int j = 0; j < P; ++j) any_walk |= walk[j] != 0;
   const int PS = P + 5;
@@ -939,10 +942,10 @@ int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const
   double* u_it = (double*)malloc(sizeof(double) * W);
   Acc acc[LANES];
   /* a-priori fit */
-  for (int64_t g = 0; g * LANES < W; ++g) {
+  for (int64_t g = 0; g * G < W; ++g) {
     integrate_group(&pb, W, g, y0, theta, NULL, acc);
-    for (int l = 0; l < LANES && g * LANES + l < W; ++l) {
-      int64_t w = g * LANES + l;
+    for (int l = 0; l < G && g * G + l < W; ++l) {
+      int64_t w = g * G + l;
       double c = acc[l].nvalid ? acc[l].chi : NAN;
       cur[w] = c;
       cur[W + w] = 1.0 - acc[l].ssres / sstot;
@@ -973,10 +976,10 @@ int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const
         y_new[(int64_t)s * W + w] = (any_walk && pi >= 0) ? th_new[(int64_t)pi * W + w] : y0[(int64_t)s * W + w];
       }
     }
-    for (int64_t g = 0; g * LANES < W; ++g) {
+    for (int64_t g = 0; g * G < W; ++g) {
       integrate_group(&pb, W, g, y_new, th_new, NULL, acc);
-      for (int l = 0; l < LANES && g * LANES + l < W; ++l) {
-        int64_t w = g * LANES + l;
+      for (int l = 0; l < G && g * G + l < W; ++l) {
+        int64_t w = g * G + l;
         double chin = acc[l].nvalid ? acc[l].chi : NAN;
         double lr = exp(cur[w] - chin);
         double accp = exp(log(lr));

@@ -31,7 +31,7 @@ def lib():
                                     i64, vp, vp, vp, vp, vp, vp, i32]
         L.ref_mh.restype = C.c_int
         L.ref_mh.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, d, d, i32, d, i32,
-                             i64, i64, i32, i32, i32, u64, d, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+                             i64, i64, i32, i32, i32, u64, d, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
         L.ref_inv_fifth_root.restype = d
         L.ref_inv_fifth_root.argtypes = [d]
         L.ref_inv_fourth_root.restype = d
@@ -112,8 +112,11 @@ def integrate(fp, y0, theta, trajectory=True, split=None):
 
 
 def mh_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, rng="philox", seed=0, replay=None,
-           step_sd=0.05, walker_offset=0):
+           step_sd=0.05, walker_offset=0, split=None):
+    """oe_mh_run restated; ``split`` as in ``integrate`` (the product's MH splits a chain over
+    the same lanes as its DOPRI5 integrate)."""
     pr = Problem(fp)
+    split = product_split(fp) if split is None else int(split)
     theta = np.array(theta, dtype=np.float64, order="C", copy=True)
     y0 = np.array(y0, dtype=np.float64, order="C", copy=True)
     W = theta.shape[1]
@@ -129,7 +132,7 @@ def mh_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, rng="philox"
         u = np.ascontiguousarray(replay[1], dtype=np.float64)
     rc = lib().ref_mh(*pr.args(), pr.sstot, pr.pnum, W, int(walker_offset), int(nits), int(burnin),
                       0 if rng == "replay" else 1, int(seed), float(step_sd), _p(walk), _p(ip), _p(dz), _p(u),
-                      _p(theta), _p(y0), _p(samples), _p(final), _p(status))
+                      _p(theta), _p(y0), _p(samples), _p(final), _p(status), split if split > 1 else 0)
     if rc:
         raise RuntimeError("ref_mh failed")
     return {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status}

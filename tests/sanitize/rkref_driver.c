@@ -19,7 +19,7 @@ int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const
            double atol, int max_steps, double sstot, int pnum, int64_t W, int64_t walker_offset, int nits, int burnin,
            int rng_mode, uint64_t seed, double step_sd, const uint8_t* walk, const int32_t* init_param,
            const double* dz, const double* uu, double* theta, double* y0, double* samples, double* final_stats,
-           int32_t* status);
+           int32_t* status, int split);
 
 static uint64_t lcg = 88172645463325252ull;
 static double unif(void) {
@@ -83,7 +83,8 @@ static void run_case(int model, int S, int P, int64_t W, int method, int with_tr
     double* fin = malloc(sizeof(double) * 4 * W);
     int32_t* mst = calloc((size_t)W, sizeof(int32_t));
     rc = ref_mh(model, S, PP, T, times, NOBS, tidx, mask, O, two_s2, lin, method, 2, 1.49012e-8, 1.49012e-8, 60,
-                1.0, PP, W, 17, nits, burnin, mode, 42, 0.05, walk, ip, dz, uu, thm, ym, samples, fin, mst);
+                1.0, PP, W, 17, nits, burnin, mode, 42, 0.05, walk, ip, dz, uu, thm, ym, samples, fin, mst,
+                split);
     if (rc) { fprintf(stderr, "ref_mh rc=%d (model %d method %d mode %d)\n", rc, model, method, mode); exit(1); }
     free(thm); free(ym); free(dz); free(uu); free(samples); free(fin); free(mst);
   }
