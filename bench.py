@@ -83,6 +83,8 @@ def parse():
                     help="run only one MCMC-leg mh_run (the PMC child pass of the MCMC roofline)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC child passes")
     ap.add_argument("--no-extra-configs", action="store_true", help="skip the C2/C3 kernel timings")
+    ap.add_argument("--no-split", action="store_true",
+                    help="wide chain models' DOPRI5: one lane per walker instead of the split kernel")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg (1 048 576 walkers over the ranks)")
     ap.add_argument("--c4-steps", type=int, default=10, help="C4 leg: timed trajectory integrates")
     return ap.parse_args()
@@ -256,12 +258,14 @@ def _cpu_worker(args):
     return done, time.perf_counter() - t0
 
 
-def cpu_baseline(model, fp, y0, budget_s, P):
+def cpu_baseline(model, fp, y0, budget_s, P, procs=None):
     """Oracle (scipy odeint, the reference's integrator) on every host core available to
     this process (``Pool(processes=cores)`` as Framework.py:779); fork-based pool started
-    before this process initialises the GPU."""
+    before this process initialises the GPU.  ``procs`` overrides the pool size
+    (tools/cpu_scaling.py: does a pool larger than the cgroup quota gain anything?)."""
     import multiprocessing as mp
     cores, detail = host_cores()
+    cores = procs or cores
     theta = synthetic_walkers(cores * 16384, P)
     jobs = [(model, fp.times, budget_s, [theta[:, w] for w in range(c, theta.shape[1], cores)], y0,
              fp.obs_tidx, fp.obs_mask, fp.obs_log, fp.obs_logsigma) for c in range(cores)]
@@ -614,7 +618,7 @@ def main():
         # back-to-back launches cost ~4 % of the C1 wall time, tools/launch_gaps.py)
         return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores,
                              sync=False, timing=False, pipelined=PIPE_ARG[args.kernel],
-                             xcd_remap=XCD_ARG[args.xcd], half_waves=args.half_waves)
+                             xcd_remap=XCD_ARG[args.xcd], half_waves=args.half_waves, split=not args.no_split)
 
     # W untimed warm-up steps, continued (in batches of 5, untimed) until at least
     # --warmup-ms of launches have run: under a kernel trace the C1 kernel runs 0.33-0.38 ms

@@ -93,6 +93,10 @@ template <class M>
 struct SplitOf { static constexpr int K = 0; };
 template <int N>
 struct SplitOf<Chain<N>> { static constexpr int K = split_lanes_chain<N>(); };
+#ifdef OE_SPLIT_TWOI  // measurement builds: two_i (Chain<4>'s RHS, operation for operation) over 2 lanes
+template <>
+struct SplitOf<TwoI> { static constexpr int K = 2; };
+#endif
 
 template <class M, int METHOD>
 void fill_method(Entry& e) {

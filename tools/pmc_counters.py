@@ -23,13 +23,19 @@ def main():
     ap.add_argument("--kernel-regex", default="k_integrate")
     ap.add_argument("--counters", nargs="+", required=True)
     ap.add_argument("--timeout", type=int, default=240)
+    ap.add_argument("--one-pass", action="store_true",
+                    help="all counters in ONE pass (the caller keeps them within one pass's block limits)")
     args, bench_args = ap.parse_known_args()
     bench_args = [a for a in bench_args if a != "--"]
-    from tools.profile import pmc_pass
+    from tools.profile import pmc_counts, pmc_pass
     out = os.path.join(ROOT, "gpurun_out", f"pmc_{args.tag}")
     os.makedirs(out, exist_ok=True)
     res = {}
-    for c in args.counters:
+    if args.one_pass:
+        r = pmc_counts(out, args.counters, bench_args + ["--no-pmc"], args.kernel_regex, args.timeout)
+        res = {c: r[c]["mean"] for c in args.counters}
+        res["dispatches"] = r[args.counters[0]]["dispatches"]
+    for c in ([] if args.one_pass else args.counters):
         try:
             r = pmc_pass(out, c, bench_args + ["--no-pmc"], args.kernel_regex, args.timeout)
             res[c] = r["mean"]

@@ -18,7 +18,8 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--walkers", type=int, default=262144)
-    ap.add_argument("--models", type=int, nargs="+", default=[10, 12, 16, 20, 24, 32])
+    ap.add_argument("--models", nargs="+", default=["10", "12", "16", "20", "24", "32"],
+                    help="chain sizes (10) or model names (two_i)")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
     args = ap.parse_args()
@@ -26,12 +27,14 @@ def main():
     import torch
     from bench import HBM_PEAK_GBS, build_problem, synthetic_walkers
     W = args.walkers
-    for n in args.models:
-        m, y0h = build_problem(f"chain{n}", "dopri5", 1000)
+    for name in args.models:
+        name = f"chain{name}" if name.isdigit() else name
+        m, y0h = build_problem(name, "dopri5", 1000)
+        n = int(y0h.shape[0])
         eng = m.engine()
         th = torch.as_tensor(synthetic_walkers(W, 5), device=eng.dev).contiguous()
         y0 = torch.as_tensor(np.repeat(y0h[:, None], W, axis=1), device=eng.dev).contiguous()
-        res = {"model": f"chain{n}", "walkers": W}
+        res = {"model": name, "walkers": W}
         for traj in (True, False):
             tr = eng.empty_traj(W) if traj else None
             for rnd in range(args.rounds):  # interleaved A/B rounds
