@@ -215,6 +215,16 @@ static double inv_fifth_root(double x) {
 
 double ref_inv_fifth_root(double x) { return inv_fifth_root(x); }
 
+/* DOPRI5 step statistics over all groups since the last reset (analysis only:
+   tools/dopri5_steps.py) -- accepted and rejected lockstep steps, groups integrated */
+static long long g_dp_stats[3];
+void ref_dopri5_stats(long long* out, int reset) {
+  for (int j = 0; j < 3; ++j) {
+    out[j] = g_dp_stats[j];
+    if (reset) g_dp_stats[j] = 0;
+  }
+}
+
 static double grp_max(Lane* L, int n, int use_dead_zero) {
   double m = 0.0;
   (void)use_dead_zero;
@@ -266,6 +276,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
   const double span = tend - t0;
   const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
   int i = 1, nst = 0, last_rej = 0;
+  long long n_acc = 0, n_rej = 0;
   while (i < pb->T) {
     int last = 0;
     if (t + h >= tend) { h = tend - t; last = 1; }
@@ -388,9 +399,11 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
       if (last_rej) fac = fmin(fac, 1.0);
       h = h * fac;
       last_rej = 0;
+      ++n_acc;
     } else {
       h = h * fmax(0.2, 0.9 * inv_fifth_root(err));
       last_rej = 1;
+      ++n_rej;
     }
     if (i < pb->T && (nst >= pb->max_steps || h < hmin)) {  /* not after the last grid point */
       for (int l = 0; l < nl; ++l)
@@ -418,6 +431,12 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     if (L[l].dead && L[l].active) L[l].a.status |= ST_MAXSTEP;
     check_finite(S, L[l].y, &L[l].a);
   }
+#pragma omp atomic
+  g_dp_stats[0] += n_acc;
+#pragma omp atomic
+  g_dp_stats[1] += n_rej;
+#pragma omp atomic
+  g_dp_stats[2] += 1;
 }
 
 
@@ -798,7 +817,7 @@ static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double*
 static Prob make_prob(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                       const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                       int substeps, double rtol, double atol, int max_steps) {
-  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol, 0};
+  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol, 0, 0};
   return pb;
 }
 

@@ -40,6 +40,8 @@ def lib():
         L.ref_philox4x32_10.argtypes = [vp, vp, vp]
         L.ref_philox_draws.restype = None
         L.ref_philox_draws.argtypes = [u64, u64, i32, i32, vp, vp]
+        L.ref_dopri5_stats.restype = None
+        L.ref_dopri5_stats.argtypes = [vp, i32]
         _lib = L
     return _lib
 
@@ -136,6 +138,13 @@ def mh_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, rng="philox"
     if rc:
         raise RuntimeError("ref_mh failed")
     return {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status}
+
+
+def dopri5_stats(reset: bool = True) -> dict:
+    """Accepted / rejected DOPRI5 lockstep steps and groups since the last reset."""
+    out = np.zeros(3, np.int64)
+    lib().ref_dopri5_stats(out.ctypes.data, int(reset))
+    return {"accepted": int(out[0]), "rejected": int(out[1]), "groups": int(out[2])}
 
 
 def inv_fifth_root(x: float) -> float:
