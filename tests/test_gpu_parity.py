@@ -402,6 +402,47 @@ def test_mh_philox_vs_c_restatement(spec, method):
     assert (dev["samples"].cpu().numpy()[:, 2, :] == theta[2]).all()  # static parameter never moves
 
 
+@pytest.mark.parametrize("n,linked", [(16, (0, 8, 15)), (24, (0, 11, 23)), (32, (0, 17, 31))])
+def test_split_mh_state0_params_vs_c_restatement(n, linked):
+    """Split DOPRI5 MH (k_mh_split: 2 lanes per chain for chain16, 4 for chain24/32):
+    '<state>0' parameters linking states held by the first, a middle and the last lane,
+    one static parameter, Philox draws — vs the C restatement, which groups 64/K chains
+    per lockstep wave as the kernel does."""
+    from odelib_amd import ModelFramework, parameter
+    from helpers import THETA, chain_rhs, demo_df
+    snames = ["S"] + [f"I{k}" for k in range(1, n - 1)] + ["V"]
+    th = dict(THETA["two_i"])
+    extra = {f"{snames[s]}0": v for s, v in zip(linked, (5236900.0, 10.0, 10981000.0))}
+    pn = list(th) + list(extra)
+    m = ModelFramework(ODE=chain_rhs(n), parameter_names=pn, state_names=snames, dataframe=demo_df({"virus": "V", "host": "H"}),
+                       state_summations={"H": snames[:-1]}, t_steps=1000, S=5236900, method="dopri5",
+                       device_model="chain", **{p: parameter(init_value=v) for p, v in {**th, **extra}.items()})
+    fp = m.fit_problem()
+    assert rk_ref.product_split(fp) == (2 if n == 16 else 4)
+    W, P = 70, len(pn)
+    theta = np.array([float(m.parameters[p].val) for p in pn])[:, None] * np.exp(
+        0.02 * np.random.RandomState(4).standard_normal((P, W)))
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    init_param = np.full(n, -1, np.int32)
+    for j, s in enumerate(linked):
+        init_param[s] = 5 + j
+    walk = np.ones(P, np.uint8)
+    walk[2] = 0
+    dev = m.engine().mh_run(theta, y0, nits=16, burnin=5, walk_mask=walk, init_param=init_param, rng="philox",
+                            seed=31, walker_offset=3)
+    ref = rk_ref.mh_run(fp, theta, y0, 16, 5, walk, init_param=init_param, rng="philox", seed=31, walker_offset=3)
+    np.testing.assert_allclose(dev["samples"].cpu().numpy(), ref["samples"], rtol=1e-8)
+    np.testing.assert_allclose(dev["theta"].cpu().numpy(), ref["theta"], rtol=1e-8)
+    np.testing.assert_allclose(dev["y0"].cpu().numpy(), ref["y0"], rtol=1e-8)
+    np.testing.assert_allclose(dev["final"].cpu().numpy(), ref["final"], rtol=1e-8)
+    assert np.array_equal(dev["status"].cpu().numpy(), ref["status"])
+    acc = dev["final"].cpu().numpy()[3]
+    assert (acc > 0).any()  # some chains moved: the linked states were exercised
+    yd, td = dev["y0"].cpu().numpy(), dev["theta"].cpu().numpy()
+    for j, s in enumerate(linked):  # a linked state follows its parameter
+        np.testing.assert_array_equal(yd[s], td[5 + j])
+
+
 def test_mh_replay_and_state0_params_vs_c_restatement():
     m, P, theta, y0 = _mh_inputs("one_i", 67, "rk4", extra={"V0": 10981000.0})
     nits = 25

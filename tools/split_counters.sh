@@ -3,7 +3,7 @@
 # --pmc pass per case (GPU box):  bash tools/split_counters.sh <tag>
 # C2: two_i 65 536 walkers, the product library (one lane) and the OE_SPLIT_TWOI
 # measurement library (alt_lib/split2, two lanes); C3-dopri5: chain20 262 144 walkers,
-# split (product) and --no-split.
+# split (product) and --no-split.  (alt_lib/ is gpurun-ignored: drop that line to rerun.)
 set -e
 tag=$1
 C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
