@@ -492,6 +492,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
     theta = opaque(theta);
     y0g = opaque(y0g);
     cur = opaque(cur);
+#if OE_MH_CHECKS
+    {  // the debug library's integrity checks, as k_mh; wave-uniform
+      bool sound = theta == ma.theta && y0g == ma.y0 && cur == ma.cur &&
+                   (it <= ma.burnin || (it - ma.row0 >= 0 && it - ma.row0 < ma.n_rows));
+#pragma unroll
+      for (int s = 0; s < N; ++s) sound = sound && ma.init_param[s] < P;
+      if (!sound) {
+        if (writer && ma.status) ma.status[w] = ST_INTERNAL;
+        return;
+      }
+    }
+#endif
     double tn[PMAX];  // the proposal again (not held in registers across the integration)
     propose(it, tn);
     const double u = Row(opaque(ma.u + (int64_t)(it - ma.draw_it0) * W), W).ld(off);

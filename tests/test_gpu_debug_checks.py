@@ -6,8 +6,8 @@ a buffer descriptor with an in-range lane offset, so a corrupted store needs a c
 wave-uniform value: a row pointer carried through the integration, the sample row index,
 or a linked-state parameter index.  The debug library checks exactly those on every
 iteration (a failed check stores nothing more and sets OE_STATUS_INTERNAL).  Here the MH
-parity cases — including the register-heaviest kernels (chain20 RK4 / DOPRI5, spilling)
-— run on the debug library against the C restatement, with no check firing; a self-test
+parity cases — including the register-heaviest kernels (chain20 RK4, chain20 DOPRI5 on
+one lane and split over two, all spilling) — run on the debug library against the C restatement, with no check firing; a self-test
 hook proves a check does fire.
 """
 import os
@@ -29,9 +29,10 @@ CHILD = textwrap.dedent(r"""
     from odelib_amd import _native as N
     from oracle import rk_ref
     selftest = bool(os.environ.get("OE_MH_CHECK_SELFTEST"))
-    cases = [("two_i", "rk4")] if selftest else [("two_i", "rk4"), ("two_i", "dopri5"), ("chain20", "rk4"),
-                                                   ("chain20", "dopri5"), ("one_i_V0", "rk4")]
-    for spec, method in cases:
+    cases = [("two_i", "rk4", True), ("chain20", "dopri5", True)] if selftest else [
+        ("two_i", "rk4", True), ("two_i", "dopri5", True), ("chain20", "rk4", True), ("chain20", "dopri5", True),
+        ("chain20", "dopri5", False), ("one_i_V0", "rk4", True)]
+    for spec, method, split in cases:
         if spec == "one_i_V0":
             m = product_model("one_i", method=method, extra_params={"V0": 10981000.0})
             init_param = [-1, -1, 4]
@@ -49,20 +50,20 @@ CHILD = textwrap.dedent(r"""
         walk = np.ones(P, np.uint8)
         walk[2] = 0
         dev = m.engine().mh_run(theta, y0, nits=30, burnin=12, walk_mask=walk, init_param=init_param,
-                                rng="philox", seed=77, walker_offset=5)
+                                rng="philox", seed=77, walker_offset=5, split=split)
         st = dev["status"].cpu().numpy()
         if selftest:
             assert (st & N.OE_STATUS_INTERNAL).all(), st
-            print("SELFTEST FIRED")
+            print("SELFTEST FIRED", spec, method)
             continue
         assert not (st & N.OE_STATUS_INTERNAL).any(), (spec, method, st)
         ref = rk_ref.mh_run(m.fit_problem(), theta, y0, 30, 12, walk, init_param=init_param, rng="philox",
-                            seed=77, walker_offset=5)
+                            seed=77, walker_offset=5, split=None if split else 1)
         tol = 1e-11 if method == "rk4" else 1e-8
         np.testing.assert_allclose(dev["samples"].cpu().numpy(), ref["samples"], rtol=tol)
         np.testing.assert_allclose(dev["final"].cpu().numpy(), ref["final"], rtol=tol)
         assert np.array_equal(st, ref["status"])
-        print("CHECKED", spec, method)
+        print("CHECKED", spec, method, "split" if split else "one lane")
     maps = open("/proc/self/maps").read()
     assert "libodelib_amd_debug.so" in maps
     print("DEBUG OK")
@@ -80,10 +81,10 @@ def test_mh_integrity_checks_hold_on_the_debug_library():
     assert os.path.exists(DEBUG_LIB), "build the debug library (make -C odelib_amd/csrc)"
     r = _run({})
     assert r.returncode == 0 and "DEBUG OK" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
-    assert r.stdout.count("CHECKED") == 5
+    assert r.stdout.count("CHECKED") == 6
 
 
 @pytest.mark.gpu
 def test_mh_integrity_check_fires_on_a_bad_row_bound():
     r = _run({"OE_MH_CHECK_SELFTEST": "1"})
-    assert r.returncode == 0 and "SELFTEST FIRED" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
+    assert r.returncode == 0 and r.stdout.count("SELFTEST FIRED") == 2, (r.stdout[-3000:], r.stderr[-3000:])
