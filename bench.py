@@ -306,6 +306,28 @@ def cpu_rk4_c(fp, y0, W, cores):
                       f"(oracle/rk_ref.c, gcc -O2, OpenMP {cores} threads), best of 2: {best:.2f} s"}
 
 
+def write_ceiling(buf, stream, launches=20, warm_ms=60.0):
+    """What this box's HBM sustains for a plain streaming write of the trajectory buffer:
+    torch's fill kernel over the same bytes, back to back, after a warm-up (untimed by the
+    metric).  The kernel's fraction of it separates the kernel from the box: the C1 kernel
+    time varies 0.335-0.379 ms between boxes of the pool with the same code."""
+    import torch
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < warm_ms:
+        buf.zero_()
+        torch.cuda.synchronize()
+    e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    e[0].record(stream)
+    for _ in range(launches):
+        buf.zero_()
+    e[1].record(stream)
+    torch.cuda.synchronize()
+    ms = e[0].elapsed_time(e[1]) / launches
+    nbytes = buf.numel() * buf.element_size()
+    return {"what": f"torch zero_() of the {nbytes / 1e9:.2f} GB trajectory buffer, {launches} back-to-back launches",
+            "ms": ms, "GB/s": nbytes / (ms / 1e3) / 1e9}
+
+
 # ------------------------------------------------------------------ GPU legs
 class Ranks:
     """This rank's device and the collectives the timing needs (barrier, max)."""
@@ -654,6 +676,7 @@ def main():
         ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     kern_dispatch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    ceiling = write_ceiling(traj, stream)
     wts = world * Wl * (T - 1) * args.steps  # walkers every rank actually ran
     value = wts / elapsed
     bytes_launch = Wl * (T - 1) * 8 * S + Wl * 8 * (S + P + 2)  # traj + y0/θ/chi/ssres
@@ -692,7 +715,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_s * 1e3, "kernel_ms_note": "timed-region event span / steps",
-                         "kernel_ms_per_dispatch": kern_dispatch_ms, "bytes_per_launch": bytes_launch},
+                         "kernel_ms_per_dispatch": kern_dispatch_ms, "bytes_per_launch": bytes_launch,
+                         "box_write_ceiling": dict(ceiling, frac_of_ceiling=achieved / ceiling["GB/s"])},
             "cpu_baseline": cpu,
             "mcmc": mcmc,
             "other_configs": extra or None,
