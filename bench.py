@@ -70,10 +70,10 @@ def parse():
     ap.add_argument("--method", default="rk4", choices=["rk4", "dopri5"])
     ap.add_argument("--times", type=int, default=1000)
     ap.add_argument("--cached-stores", action="store_true", help="plain (cached) trajectory stores")
-    ap.add_argument("--kernel", default="direct", choices=["direct", "pipe2", "pipe4", "pipe8"],
-                    help="RK4 trajectory kernel (A/B of the opt-in producer/consumer variants)")
-    ap.add_argument("--half-waves", action="store_true",
-                    help="32 walkers per wavefront in the headline RK4 kernel (same bits; A/B)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "half", "pipe2", "pipe4", "pipe8"],
+                    help="RK4 trajectory kernel: auto = the library times the bitwise-identical kernels on "
+                         "this device (OE_TUNE, during the warm-up) and keeps the fastest; or a fixed one (A/B)")
+    ap.add_argument("--half-waves", action="store_true", help="same as --kernel half")
     ap.add_argument("--xcd", default="runs", choices=["runs", "ranges", "off"],
                     help="walker blocks per XCD: runs of 512 walkers (default), one range, blockIdx order")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (wall seconds)")
@@ -177,7 +177,6 @@ def pmc_mh_flops(args):
         return None, f"PMC pass failed: {e!r}"[:200]
 
 
-PIPE_ARG = {"direct": False, "pipe2": 2, "pipe4": 4, "pipe8": 8}
 XCD_ARG = {"runs": True, "ranges": "ranges", "off": False}
 
 
@@ -460,7 +459,8 @@ def c4_leg(args, R, T, P):
     traj = eng.empty_traj(cnt)
 
     def step():
-        return eng.integrate(y0, theta, trajectory=True, traj_out=traj, sync=False, timing=False)
+        return eng.integrate(y0, theta, trajectory=True, traj_out=traj, sync=False, timing=False,
+                             kernel="half" if args.half_waves else args.kernel)
     warm(step)
     K = args.c4_steps
     R.fence()
@@ -474,7 +474,7 @@ def c4_leg(args, R, T, P):
     R.fence()
     wall, kms = R.max(time.perf_counter() - t0, ev[0].elapsed_time(ev[1]) / K)
     res["integrate"] = {"steps": K, "ms_per_step": wall / K * 1e3, "kernel_ms_max_rank": kms,
-                        "walker_timesteps_per_s": C4_WALKERS * (T - 1) * K / wall,
+                        "walker_timesteps_per_s": C4_WALKERS * (T - 1) * K / wall, "kernel": eng.last_variant(),
                         "hbm_frac_per_gpu": cnt * (T - 1) * 8 * S / (kms / 1e3) / 1e9 / HBM_PEAK_GBS,
                         "chi_finite": bool(torch.isfinite(out["chi"]).all().item())}
     del traj, out
@@ -538,6 +538,7 @@ def extra_configs(args, R, T, P):
             ("C3-dopri5-onelane", "chain20", "dopri5", 262144, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"))
     for name, model, method, W, stiff, subs, tol in cfgs:
         split = not name.endswith("-onelane")
+        kern = ("half" if args.half_waves else args.kernel) if method == "rk4" else None
         ex, y0x = R.engine(model, method, T, subs)
         Sx = len(y0x)
         thh = synthetic_walkers(W, P)
@@ -553,13 +554,13 @@ def extra_configs(args, R, T, P):
         # without event markers, timed by two events on the stream
         K = 20 if not n_stiff else 3
         warm(lambda: ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False,
-                                  xcd_remap=XCD_ARG[args.xcd], split=split))
+                                  xcd_remap=XCD_ARG[args.xcd], split=split, kernel=kern))
         sx = torch.cuda.current_stream(R.dev)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record(sx)
         for _ in range(K):
             outx = ex.integrate(y0t, thx, trajectory=True, traj_out=trx, sync=False, timing=False,
-                                xcd_remap=XCD_ARG[args.xcd], split=split)
+                                xcd_remap=XCD_ARG[args.xcd], split=split, kernel=kern)
         ev[1].record(sx)
         torch.cuda.synchronize(R.dev)
         kms = ev[0].elapsed_time(ev[1]) / K
@@ -571,6 +572,7 @@ def extra_configs(args, R, T, P):
                        "hbm_frac": byt / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "tolerance": tol}
         if method == "rk4":
             extra[name]["rk4_substeps"] = subs
+            extra[name]["kernel"] = ex.last_variant()
         if model == "chain20" and method == "dopri5":
             extra[name]["lanes_per_walker"] = 2 if split else 1
         if n_stiff:
@@ -634,13 +636,14 @@ def main():
         return
 
     traj = eng.empty_traj(Wl)
+    kernel = "half" if args.half_waves else args.kernel
 
     def step():
         # no timing-event markers between the timed launches (measured: markers between
         # back-to-back launches cost ~4 % of the C1 wall time, tools/launch_gaps.py)
         return eng.integrate(y0, theta, trajectory=True, traj_out=traj, nt_stores=not args.cached_stores,
-                             sync=False, timing=False, pipelined=PIPE_ARG[args.kernel],
-                             xcd_remap=XCD_ARG[args.xcd], half_waves=args.half_waves, split=not args.no_split)
+                             sync=False, timing=False, kernel=kernel,
+                             xcd_remap=XCD_ARG[args.xcd], split=not args.no_split)
 
     # W untimed warm-up steps, continued (in batches of 5, untimed) until at least
     # --warmup-ms of launches have run: under a kernel trace the C1 kernel runs 0.33-0.38 ms
@@ -676,6 +679,8 @@ def main():
         ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     kern_dispatch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    ran = eng.last_variant()
+    tune = eng.tune_times() if kernel == "auto" else None
     ceiling = write_ceiling(traj, stream)
     wts = world * Wl * (T - 1) * args.steps  # walkers every rank actually ran
     value = wts / elapsed
@@ -709,7 +714,7 @@ def main():
                        "method": args.method, "rk4_substeps": 1,
                        "tolerance": "vs tight odeint: rtol 1e-6, atol 1e-6 (test-pinned)",
                        "stores": "cached" if args.cached_stores else "nontemporal",
-                       "kernel": args.kernel + ("-half" if args.half_waves else ""), "xcd": args.xcd,
+                       "kernel": ran, "kernel_choice": kernel, "kernel_tune_ms": tune, "xcd": args.xcd,
                        "parallelism": f"walker-shard x{world}",
                        "launch": "torchrun, one rank per GPU" if world > 1 else "single process"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define OE_ABI_VERSION 4
+#define OE_ABI_VERSION 5
 
 /* return codes */
 enum {
@@ -109,11 +109,30 @@ enum {
   OE_PIPE_8 = 1024u,
   OE_XCD_RANGES = 2048u, /* oe_integrate: one contiguous walker range per XCD instead (the r01
                            mapping; same results) */
-  OE_NO_SPLIT = 4096u   /* oe_integrate / oe_mh_run, OE_METHOD_DOPRI5: one lane per walker even for the models
+  OE_NO_SPLIT = 4096u,  /* oe_integrate / oe_mh_run, OE_METHOD_DOPRI5: one lane per walker even for the models
                            whose DOPRI5 kernel splits a walker over K lanes (built-in chain with
                            14..22 states: K = 2; 24+ states, a multiple of 4: K = 4).  A split
                            wave holds 64/K walkers, which share one step size, so results differ
                            from the one-lane grouping (64 walkers per step size) within tolerance */
+  OE_TUNE = 8192u       /* oe_integrate, OE_METHOD_RK4 with a trajectory: pick the fastest of the
+                           RK4 trajectory kernels (OE_KERNEL_*; all produce the same bits) for this
+                           shape on this device.  The first call for a shape (model, W, T,
+                           substeps, store policy, XCD order) runs each candidate back to back
+                           after ~60 ms of launches (the clock settles), three interleaved rounds,
+                           and keeps the fastest (the default kernel unless another is > 1 %
+                           faster); later calls reuse the choice.  The first call synchronizes
+                           the stream.  Overrides OE_PIPE*, OE_HALF_WAVES. */
+};
+
+/* RK4 trajectory kernels (oe_last_variant; all bitwise identical) */
+enum {
+  OE_KERNEL_DIRECT = 0, /* one walker per lane, 64 walkers per wavefront, stores from the compute waves */
+  OE_KERNEL_HALF = 1,   /* 32 walkers per wavefront (OE_HALF_WAVES) */
+  OE_KERNEL_PIPE2 = 2,  /* producer/consumer: 4 compute waves + 2 / 4 / 8 store waves per workgroup */
+  OE_KERNEL_PIPE4 = 3,  /*   through an LDS ring (OE_PIPE / OE_PIPE_4 / OE_PIPE_8) */
+  OE_KERNEL_PIPE8 = 4,
+  OE_KERNEL_OTHER = 5,  /* not an RK4 trajectory launch (DOPRI5, stiff, no trajectory, MH) */
+  OE_KERNEL_COUNT = 6
 };
 
 /* RNG modes for oe_mh_run */
@@ -263,6 +282,13 @@ int oe_allgather_samples(oe_comm* comm, int64_t rows, const double* block, const
 /* Device time (ms) of the kernel launches of the last oe_integrate / oe_mh_run,
  * from HIP events recorded on the context's stream around them (waits for them). */
 int oe_last_kernel_ms(oe_ctx* ctx, double* ms);
+
+/* The kernel (OE_KERNEL_*) the last oe_integrate launched.  OE_ERR_STATE before any call. */
+int oe_last_variant(oe_ctx* ctx, int32_t* variant);
+/* OE_TUNE's measurements for the shape of the last oe_integrate: ms[k] = mean launch time of
+ * kernel k (back to back, best of the rounds), NaN for kernels not measured (not available for
+ * the shape).  n >= OE_KERNEL_COUNT - 1 entries.  OE_ERR_STATE if that call was not tuned. */
+int oe_tune_times(oe_ctx* ctx, double* ms, int32_t n);
 
 #ifdef __cplusplus
 }

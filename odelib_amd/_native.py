@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ODELIB_AMD_LIB", os.path.join(_HERE, "csrc", "libodelib_amd.so"))
 
 # --- constants mirrored from include/odelib_amd.h -----------------------------------
-OE_ABI_VERSION = 4
+OE_ABI_VERSION = 5
 OE_COMM_ID_BYTES = 128
 OE_OK = 0
 OE_ERR_ARG, OE_ERR_HIP, OE_ERR_STATE, OE_ERR_UNSUPPORTED, OE_ERR_NOMEM = -1, -2, -3, -4, -5
@@ -24,7 +24,10 @@ OE_MODEL_ZERO_I, OE_MODEL_ONE_I, OE_MODEL_TWO_I, OE_MODEL_CHAIN = 0, 1, 2, 3
 OE_MODEL_CUSTOM = 1000
 OE_STATUS_NONFINITE, OE_STATUS_NEGATIVE, OE_STATUS_MAXSTEP, OE_STATUS_STIFF, OE_STATUS_INTERNAL = 1, 2, 4, 8, 16
 OE_HOST_PTRS, OE_ASYNC, OE_NT_STORES, OE_PIPE, OE_HALF_WAVES, OE_NO_XCD_REMAP, OE_NO_TIMING = 1, 2, 4, 8, 16, 64, 128
-OE_PIPE_4, OE_PIPE_8, OE_XCD_RANGES, OE_NO_SPLIT = 512, 1024, 2048, 4096
+OE_PIPE_4, OE_PIPE_8, OE_XCD_RANGES, OE_NO_SPLIT, OE_TUNE = 512, 1024, 2048, 4096, 8192
+OE_KERNEL_DIRECT, OE_KERNEL_HALF, OE_KERNEL_PIPE2, OE_KERNEL_PIPE4, OE_KERNEL_PIPE8, OE_KERNEL_OTHER = range(6)
+OE_KERNEL_COUNT = 6
+KERNEL_NAMES = ("direct", "half", "pipe2", "pipe4", "pipe8", "other")
 OE_RNG_REPLAY, OE_RNG_PHILOX, OE_RNG_NUMPY = 0, 1, 2
 
 # every symbol include/odelib_amd.h declares (checked by tests/test_abi.py)
@@ -49,6 +52,8 @@ EXPORTED = (
     "oe_comm_last_error",
     "oe_comm_set_stream",
     "oe_allgather_samples",
+    "oe_last_variant",
+    "oe_tune_times",
 )
 
 
@@ -172,6 +177,10 @@ def load_library(path: str | None = None):
         lib.oe_comm_set_stream.argtypes = [vp, vp]
         lib.oe_allgather_samples.restype = C.c_int
         lib.oe_allgather_samples.argtypes = [vp, i64, vp, vp, vp, u32]
+        lib.oe_last_variant.restype = C.c_int
+        lib.oe_last_variant.argtypes = [vp, C.POINTER(i32)]
+        lib.oe_tune_times.restype = C.c_int
+        lib.oe_tune_times.argtypes = [vp, C.POINTER(C.c_double), i32]
         if lib.oe_abi_version() != OE_ABI_VERSION:
             raise NativeUnavailable("libodelib_amd.so ABI version mismatch; rebuild it")
         if path is None:
@@ -249,6 +258,19 @@ class Context:
         ms = C.c_double(0.0)
         self._check(self.lib.oe_last_kernel_ms(self._h, C.byref(ms)), "oe_last_kernel_ms")
         return ms.value
+
+    def last_variant(self) -> int:
+        """OE_KERNEL_* of the last oe_integrate."""
+        v = C.c_int32(-1)
+        self._check(self.lib.oe_last_variant(self._h, C.byref(v)), "oe_last_variant")
+        return v.value
+
+    def tune_times(self) -> dict:
+        """OE_TUNE's per-kernel ms for the last oe_integrate's shape (measured kernels only)."""
+        n = OE_KERNEL_COUNT - 1
+        buf = (C.c_double * n)()
+        self._check(self.lib.oe_tune_times(self._h, buf, n), "oe_tune_times")
+        return {KERNEL_NAMES[k]: buf[k] for k in range(n) if buf[k] == buf[k]}
 
     def close(self):
         if self._h and self._h.value:

@@ -97,6 +97,18 @@ struct oe_ctx {
   size_t np_state_bytes = 0;
   int32_t* stiff_buf = nullptr;  // wide-model stiff redo: [count][list W][status W]
   size_t stiff_cap = 0;          // walkers it holds
+  // OE_TUNE: the RK4 trajectory kernel chosen per shape, with what was measured
+  struct Tuned {
+    const Entry* e;
+    int64_t W;
+    int32_t T, substeps;
+    uint32_t mode;  // nt | xcd flags
+    int32_t variant;
+    double ms[OE_KERNEL_COUNT - 1];
+  };
+  std::vector<Tuned> tuned;
+  int32_t last_variant = -1;
+  int32_t last_tuned = -1;  // index into tuned of the last oe_integrate, or -1
 };
 
 namespace {
@@ -206,6 +218,98 @@ struct DeviceGuard {
   DeviceGuard device_guard_((ctx)->device);                                               \
   if (device_guard_.err != hipSuccess)                                                    \
     return fail(ctx, OE_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(device_guard_.err))
+
+// XCD walker runs of the one-lane kernels: 512 consecutive walkers (4 KiB of each state
+// row) per XCD in turn (OE_XCD_RUN_WALKERS overrides, for measurements), or one contiguous
+// range per XCD, or blockIdx order
+int32_t xcd_remap_of(uint32_t flags, const dim3& grid, int64_t per_block) {
+  static const int64_t run_walkers = [] {
+    const char* v = getenv("OE_XCD_RUN_WALKERS");
+    const long n = v ? strtol(v, nullptr, 10) : 0;
+    return n > 0 ? (int64_t)n : (int64_t)512;
+  }();
+  return (flags & OE_NO_XCD_REMAP) ? 0
+         : (flags & OE_XCD_RANGES) ? (int32_t)std::max<int64_t>(1, (int64_t)grid.x / 8)
+                                   : (int32_t)std::max<int64_t>(1, run_walkers / per_block);
+}
+
+// an RK4 trajectory kernel (OE_KERNEL_*) available for this entry and walker count
+bool rk4_variant_ok(const Entry* e, int64_t W, int variant, bool nt) {
+  if (variant == OE_KERNEL_DIRECT || variant == OE_KERNEL_HALF) return true;
+  if (variant < OE_KERNEL_PIPE2 || variant > OE_KERNEL_PIPE8) return false;
+  return !e->rtc && W % 2 == 0 && e->rk4_piped[variant - OE_KERNEL_PIPE2][nt ? 1 : 0] != nullptr;
+}
+
+// one RK4 trajectory launch with the given kernel (same bits for every variant)
+hipError_t launch_rk4_traj(oe_ctx* c, const Entry* e, IntegrateArgs ia, int variant, bool nt, uint32_t flags) {
+  const int64_t W = ia.W;
+  if (variant >= OE_KERNEL_PIPE2) {
+    const int pv = variant - OE_KERNEL_PIPE2;
+    const dim3 grid((unsigned)((W + kPipeWalkers - 1) / kPipeWalkers)), block(256 + 64 * (2 << pv));
+    e->rk4_piped[pv][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
+    return hipGetLastError();
+  }
+  ia.half = variant == OE_KERNEL_HALF ? 1 : 0;
+  const int64_t per_block = ia.half ? kBlock / 2 : kBlock;
+  const dim3 grid((unsigned)((W + per_block - 1) / per_block)), block(kBlock);
+  ia.xcd_remap = xcd_remap_of(flags, grid, per_block);
+  return launch_integrate_entry(e, OE_METHOD_RK4, 1, nt ? 1 : 0, c->dp, ia, grid, block, c->stream);
+}
+
+// OE_TUNE: time every available RK4 trajectory kernel for this shape, back to back, after
+// the clock has settled under load, and remember the fastest.  Returns the cache index.
+int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32_t flags, int dflt, int* idx) {
+  const uint32_t mode = (nt ? 1u : 0u) | (flags & (OE_NO_XCD_REMAP | OE_XCD_RANGES));
+  for (size_t i = 0; i < c->tuned.size(); ++i) {
+    const oe_ctx::Tuned& t = c->tuned[i];
+    if (t.e == e && t.W == ia.W && t.T == c->dp.T && t.substeps == c->dp.substeps && t.mode == mode) {
+      *idx = (int)i;
+      return OE_OK;
+    }
+  }
+  constexpr int kN = OE_KERNEL_COUNT - 1;
+  std::vector<int> cand;
+  for (int v = 0; v < kN; ++v)
+    if (rk4_variant_ok(e, ia.W, v, nt)) cand.push_back(v);
+  auto batch = [&](int v, int n, float* ms) -> int {
+    OE_HIP(c, hipEventRecord(c->ev0, c->stream));
+    for (int k = 0; k < n; ++k) OE_HIP(c, launch_rk4_traj(c, e, ia, v, nt, flags));
+    OE_HIP(c, hipEventRecord(c->ev1, c->stream));
+    OE_HIP(c, hipEventSynchronize(c->ev1));
+    OE_HIP(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return OE_OK;
+  };
+  // settle: >= 60 ms of back-to-back launches of the default kernel (the clock and power
+  // management take tens of ms to reach the sustained state)
+  float ms = 0.f;
+  int rc = batch(dflt, 1, &ms);
+  if (rc) return rc;
+  const int per = ms > 4.f ? 2 : 8;  // launches per measurement
+  for (double settled = ms; settled < 60.0;) {
+    rc = batch(dflt, per, &ms);
+    if (rc) return rc;
+    settled += ms;
+  }
+  oe_ctx::Tuned t{e, ia.W, c->dp.T, c->dp.substeps, mode, dflt, {}};
+  for (int v = 0; v < kN; ++v) t.ms[v] = HUGE_VAL;
+  constexpr int kRounds = 3;
+  for (int r = 0; r < kRounds; ++r)
+    for (size_t j = 0; j < cand.size(); ++j) {
+      const int v = cand[(j + r) % cand.size()];  // rotate the order between rounds
+      rc = batch(v, per, &ms);
+      if (rc) return rc;
+      t.ms[v] = std::min(t.ms[v], (double)ms / per);
+    }
+  int best = dflt;
+  for (int v : cand)
+    if (t.ms[v] < 0.99 * t.ms[dflt] && t.ms[v] < t.ms[best]) best = v;
+  for (int v = 0; v < kN; ++v)
+    if (t.ms[v] == HUGE_VAL) t.ms[v] = std::nan("");
+  t.variant = best;
+  c->tuned.push_back(t);
+  *idx = (int)c->tuned.size() - 1;
+  return OE_OK;
+}
 
 }  // namespace
 
@@ -512,23 +616,37 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     ia.y0 = y0; ia.theta = theta; ia.traj = traj; ia.chi = chi; ia.ssres = ssres; ia.status = status;
   }
 
-  // Opt-in producer/consumer RK4 trajectory kernel (4 compute waves hand each row to 2, 4
-  // or 8 dedicated store waves through a 128 KiB LDS ring; 16-B stores; needs W even).
-  // Isolated launches run faster than the direct kernel (C1 0.365 vs 0.396 ms: part of
-  // the 2.1 GB stays dirty in the 256 MB MALL when the launch ends), back-to-back
-  // launches — the bench — do not (0.3995 vs 0.3912 ms): both then sit at the sustained
-  // store rate of the chip, so it is not the default.
-  int pipe_v = -1;
-  if (flags & OE_PIPE_8) pipe_v = 2;
-  else if (flags & OE_PIPE_4) pipe_v = 1;
-  else if (flags & OE_PIPE) pipe_v = 0;
-  const bool piped = pipe_v >= 0 && !e->rtc && c->method == OE_METHOD_RK4 && ia.traj && (W % 2 == 0) &&
-                     e->rk4_piped[pipe_v][nt ? 1 : 0];
+  // RK4 trajectories: one of the bitwise-identical kernels (OE_KERNEL_*).
+  // * direct: 64 walkers per wave; by default, except:
+  // * half: 32 walkers per wave (twice the storing waves).  At <= 1 wave per SIMD a trajectory
+  //   of 5+ states is store-issue bound, so the library takes it there (65 536 walkers: chain5
+  //   0.508 -> 0.474 ms, chain6 0.694 -> 0.576, chain8 0.89 -> 0.77; two_i 0.394 vs 0.401).
+  // * pipe2/4/8 (opt-in): 4 compute waves hand each row to 2, 4 or 8 store waves through a
+  //   128 KiB LDS ring, 16-B stores; W even.  Which of these wins back to back differs from
+  //   box to box (C1: pipe4 0.349 vs direct 0.379 ms on one box, 0.400 vs 0.391 on another;
+  //   DESIGN.md §6), hence OE_TUNE, which measures them on the device at hand.
+  const bool rk4_traj = c->method == OE_METHOD_RK4 && ia.traj;
+  int variant = OE_KERNEL_OTHER;
+  c->last_tuned = -1;
+  if (rk4_traj) {
+    const bool auto_half = S >= 5 && W <= (int64_t)64 * 4 * c->n_cu;
+    const int dflt = ((flags & OE_HALF_WAVES) || auto_half) ? OE_KERNEL_HALF : OE_KERNEL_DIRECT;
+    const int asked = (flags & OE_PIPE_8) ? OE_KERNEL_PIPE8 : (flags & OE_PIPE_4) ? OE_KERNEL_PIPE4
+                      : (flags & OE_PIPE) ? OE_KERNEL_PIPE2 : dflt;
+    variant = rk4_variant_ok(e, W, asked, nt) ? asked : dflt;
+    if (flags & OE_TUNE) {
+      int idx = -1;
+      rc = tune_rk4(c, e, ia, nt, flags, dflt, &idx);
+      if (rc) return rc;
+      variant = c->tuned[idx].variant;
+      c->last_tuned = idx;
+    }
+  }
+  c->last_variant = variant;
   const bool timing = !(flags & OE_NO_TIMING);
   if (timing) OE_HIP(c, hipEventRecord(c->ev0, c->stream));
-  if (piped) {
-    const dim3 grid((unsigned)((W + kPipeWalkers - 1) / kPipeWalkers)), block(256 + 64 * (2 << pipe_v));
-    e->rk4_piped[pipe_v][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
+  if (rk4_traj) {
+    OE_HIP(c, launch_rk4_traj(c, e, ia, variant, nt, flags));
   } else if (c->method == OE_METHOD_DOPRI5 && !e->rtc && e->split_lanes > 0 && !(flags & OE_NO_SPLIT)) {
     // wide chain models: one walker over K adjacent lanes (split.cuh), blocks of 256/K
     // walkers dealt to the XCDs in runs of 512 walkers as the one-lane kernel's
@@ -541,26 +659,13 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
                                              : (int32_t)std::max<int64_t>(1, 512 / per_block);
     e->dopri5_split[ia.traj ? 1 : 0][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
   } else {
-    // RK4 trajectories of 5+ states at <= 1 wave per SIMD are store-issue bound: run
-    // 32 walkers per wave (twice the storing waves; same bits).  Measured on MI355X at
-    // 65536 walkers: chain5 0.508 -> 0.474 ms, chain6 0.694 -> 0.576, chain8 0.89 ->
-    // 0.77; two_i (4 states) 0.394 vs 0.401, so full waves there.  DOPRI5 keeps 64-lane
-    // groups (its step size is shared per wave).
+    // RK4 without a trajectory (32 walkers per wave only on request), DOPRI5 (64-lane
+    // groups: its step size is shared per wave), the stiff methods
     const bool rk4 = c->method == OE_METHOD_RK4;
-    const bool auto_half = rk4 && ia.traj && S >= 5 && W <= (int64_t)64 * 4 * c->n_cu;
-    ia.half = (rk4 && ((flags & OE_HALF_WAVES) || auto_half)) ? 1 : 0;
+    ia.half = (rk4 && (flags & OE_HALF_WAVES)) ? 1 : 0;
     const int64_t per_block = ia.half ? kBlock / 2 : kBlock;
     const dim3 grid((unsigned)((W + per_block - 1) / per_block)), block(kBlock);
-    // XCD runs of 512 walkers (4 KiB of each state row; OE_XCD_RUN_WALKERS overrides, for
-    // measurements), or one contiguous range per XCD
-    static const int64_t run_walkers = [] {
-      const char* v = getenv("OE_XCD_RUN_WALKERS");
-      const long n = v ? strtol(v, nullptr, 10) : 0;
-      return n > 0 ? (int64_t)n : (int64_t)512;
-    }();
-    ia.xcd_remap = (flags & OE_NO_XCD_REMAP) ? 0
-                   : (flags & OE_XCD_RANGES) ? (int32_t)std::max<int64_t>(1, (int64_t)grid.x / 8)
-                                             : (int32_t)std::max<int64_t>(1, run_walkers / per_block);
+    ia.xcd_remap = xcd_remap_of(flags, grid, per_block);
     // Models wider than the register-resident stiff path: 'auto' marks the walkers the
     // DOPRI5 pass evicts, and k_stiff_wave redoes them one wave per walker; 'rosenbrock'
     // is k_stiff_wave for every walker (stiff_wave.cuh).
@@ -812,6 +917,21 @@ int oe_last_kernel_ms(oe_ctx* c, double* ms) {
   float f = 0.f;
   OE_HIP(c, hipEventElapsedTime(&f, c->ev0, c->ev1));
   *ms = (double)f;
+  return OE_OK;
+}
+
+int oe_last_variant(oe_ctx* c, int32_t* variant) {
+  if (!c || !variant) return OE_ERR_ARG;
+  if (c->last_variant < 0) return fail(c, OE_ERR_STATE, "oe_last_variant: no oe_integrate yet");
+  *variant = c->last_variant;
+  return OE_OK;
+}
+
+int oe_tune_times(oe_ctx* c, double* ms, int32_t n) {
+  if (!c || !ms || n < OE_KERNEL_COUNT - 1) return OE_ERR_ARG;
+  if (c->last_tuned < 0) return fail(c, OE_ERR_STATE, "oe_tune_times: the last oe_integrate was not tuned");
+  const oe_ctx::Tuned& t = c->tuned[c->last_tuned];
+  for (int v = 0; v < OE_KERNEL_COUNT - 1; ++v) ms[v] = t.ms[v];
   return OE_OK;
 }
 

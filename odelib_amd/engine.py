@@ -247,7 +247,7 @@ class Engine:
     # -- batched integrate -------------------------------------------------------------------
     def integrate(self, y0, theta, trajectory: bool = True, traj_out=None, nt_stores: bool = True,
                   sync: bool = True, pipelined=None, half_waves: bool = False,
-                  xcd_remap=True, timing: bool = True, split: bool = True):
+                  xcd_remap=True, timing: bool = True, split: bool = True, kernel=None):
         """y0 [S][W], theta [P][W] → dict(traj [T][S][W] | None, chi [W], ssres [W], status [W]).
 
         ``pipelined=True`` (or 2, 4, 8: store waves per 4 compute waves) selects the
@@ -258,8 +258,19 @@ class Engine:
         contiguous walker range (same results either way).  ``timing=False`` records no library events
         around the launch (``last_kernel_ms`` is then unavailable for this call).
         ``split=False`` keeps one lane per walker in DOPRI5 for the models whose kernel
-        otherwise spreads a walker over 2 or 4 lanes (OE_NO_SPLIT; the wide built-in chain)."""
+        otherwise spreads a walker over 2 or 4 lanes (OE_NO_SPLIT; the wide built-in chain).
+        ``kernel`` names the RK4 trajectory kernel instead: "direct" (the library's default
+        rule: 32 walkers per wave for 5+ states at <= 1 wave per SIMD), "half", "pipe2",
+        "pipe4", "pipe8", or "auto" (OE_TUNE: the library measures the available ones for
+        this shape on the first call and keeps the fastest; ``last_variant()`` says which
+        ran).  All of them produce the same bits."""
         torch = self.torch
+        if kernel is not None:
+            if kernel not in ("auto", "direct", "half", "pipe2", "pipe4", "pipe8"):
+                raise ValueError(f"unknown kernel {kernel!r}")
+            if kernel != "auto":
+                pipelined = {"direct": False, "half": False, "pipe2": 2, "pipe4": 4, "pipe8": 8}[kernel]
+                half_waves = (kernel == "half")
         pb = self.problem
         theta_t = theta if isinstance(theta, torch.Tensor) else np.asarray(theta)
         W = int(theta_t.shape[1])
@@ -279,7 +290,8 @@ class Engine:
         flags = N.OE_ASYNC | (N.OE_NT_STORES if nt_stores else 0) | pipe \
             | (N.OE_HALF_WAVES if half_waves else 0) \
             | (N.OE_XCD_RANGES if xcd_remap == "ranges" else 0 if xcd_remap else N.OE_NO_XCD_REMAP) \
-            | (0 if timing else N.OE_NO_TIMING) | (0 if split else N.OE_NO_SPLIT)
+            | (0 if timing else N.OE_NO_TIMING) | (0 if split else N.OE_NO_SPLIT) \
+            | (N.OE_TUNE if kernel == "auto" else 0)
         self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)
         if sync:
             torch.cuda.synchronize(self.dev)
@@ -287,6 +299,15 @@ class Engine:
 
     def last_kernel_ms(self) -> float:
         return self.ctx.last_kernel_ms()
+
+    def last_variant(self) -> str:
+        """Name of the kernel the last ``integrate`` launched ("direct", "half", "pipe2",
+        "pipe4", "pipe8"; "other" for DOPRI5, the stiff methods, no trajectory)."""
+        return N.KERNEL_NAMES[self.ctx.last_variant()]
+
+    def tune_times(self) -> dict:
+        """What ``kernel="auto"`` measured for the last ``integrate``'s shape: ms per kernel."""
+        return self.ctx.tune_times()
 
     # -- batched Metropolis–Hastings ---------------------------------------------------------
     def numpy_streams(self, seeds, nits: int, walk_mask, prior_draws: int = 0, step_sd: float = 0.05):

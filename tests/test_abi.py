@@ -56,6 +56,10 @@ def test_errors_are_codes_not_crashes():
     assert lib.oe_last_error(None) == b"null context"
     ms = C.c_double()
     assert lib.oe_last_kernel_ms(None, C.byref(ms)) == -1
+    v = C.c_int32()
+    assert lib.oe_last_variant(None, C.byref(v)) == -1
+    buf = (C.c_double * 5)()
+    assert lib.oe_tune_times(None, buf, 5) == -1
     s, p = C.c_int32(0), C.c_int32(0)
     assert lib.oe_model_info(99, C.byref(s), C.byref(p)) == -4
     # the pooling entry points validate before touching RCCL or the device

@@ -82,6 +82,37 @@ def test_rk4_pipelined_kernel_matches_direct_kernel(spec, W):
         assert np.array_equal(c["traj"].cpu().numpy(), b["traj"].cpu().numpy())
 
 
+@pytest.mark.parametrize("spec", ["two_i", "chain5", "chain20"])
+@pytest.mark.parametrize("W", [7, 4098])
+def test_rk4_tuned_kernel_choice(spec, W):
+    """kernel="auto" (OE_TUNE): the library times the available RK4 trajectory kernels for
+    the shape, keeps the fastest, reuses the choice, and the result is the bits of the
+    default kernel and of the C restatement.  Odd W and S > 8 have no piped kernel."""
+    m = _model(spec, "rk4")
+    theta = _walkers(spec, W)
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    eng = m.engine()
+    b = eng.integrate(y0, theta)
+    assert eng.last_variant() in ("direct", "half")
+    a = eng.integrate(y0, theta, kernel="auto")
+    tuned = eng.tune_times()
+    chosen = eng.last_variant()
+    assert chosen in tuned and set(tuned) >= {"direct", "half"}
+    assert all(0 < v < 1e3 for v in tuned.values()), tuned
+    piped = {"pipe2", "pipe4", "pipe8"} & set(tuned)
+    assert piped == (set() if (W % 2 or int(spec[5:] if spec.startswith("chain") else 4) > 8)
+                     else {"pipe2", "pipe4", "pipe8"})
+    for key in ("traj", "chi", "ssres", "status"):
+        assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
+    c = eng.integrate(y0, theta, kernel="auto")  # cached: same choice, same numbers reported
+    assert eng.last_variant() == chosen and eng.tune_times() == tuned
+    assert np.array_equal(c["traj"].cpu().numpy(), rk_ref.integrate(m.fit_problem(), y0, theta)["traj"])
+    eng.integrate(y0, theta, kernel="auto", trajectory=False)
+    assert eng.last_variant() == "other"
+    with pytest.raises(RuntimeError):
+        eng.tune_times()
+
+
 @pytest.mark.parametrize("spec", ["two_i", "chain8", "chain20"])
 @pytest.mark.parametrize("W", [1, 33, 4099])
 def test_rk4_half_waves_match_full_waves(spec, W):
