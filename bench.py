@@ -149,9 +149,24 @@ def pmc_traffic(args):
         wl = workload_args(args) + ["--no-pmc"]
         f = pmc_pass(out, "FETCH_SIZE", wl, "k_integrate", 240)
         w = pmc_pass(out, "WRITE_SIZE", wl, "k_integrate", 240)
-        return f["mean"] * 1024 * 2 + w["mean"] * 1024, f"rocprofv3 PMC FETCH_SIZE(x2)+WRITE_SIZE, {f['dispatches']} dispatches"
+        # per kernel (with --kernel auto the child runs every candidate while it tunes)
+        by = {n: {"bytes": f["by_kernel"][n]["mean"] * 1024 * 2 + w["by_kernel"][n]["mean"] * 1024,
+                  "dispatches": f["by_kernel"][n]["dispatches"]}
+              for n in f["by_kernel"] if n in w["by_kernel"]}
+        return by, "rocprofv3 PMC FETCH_SIZE(x2)+WRITE_SIZE, separate passes, per dispatch of the kernel that ran"
     except BaseException as e:  # never let profiling break the bench line
         return None, f"PMC pass failed: {e!r}"[:200]
+
+
+def traffic_of(by_kernel, variant, method):
+    """The PMC bytes per dispatch of the kernel the timed region ran (by demangled name)."""
+    if not by_kernel:
+        return None
+    meth = {"rk4": 0, "dopri5": 1}[method]
+    want = (("k_integrate_rk4_piped<", f", true, {variant[4:]}>") if variant.startswith("pipe")
+            else ("k_integrate<", f", {meth}, true, true>"))
+    hits = [v["bytes"] for n, v in by_kernel.items() if all(x in n for x in want)]
+    return hits[0] if hits else None
 
 
 def pmc_mh_flops(args):
@@ -718,7 +733,8 @@ def main():
                        "parallelism": f"walker-shard x{world}",
                        "launch": "torchrun, one rank per GPU" if world > 1 else "single process"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_of(traffic, ran, args.method),
+                         "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_s * 1e3, "kernel_ms_note": "timed-region event span / steps",
                          "kernel_ms_per_dispatch": kern_dispatch_ms, "bytes_per_launch": bytes_launch,
                          "box_write_ceiling": dict(ceiling, frac_of_ceiling=achieved / ceiling["GB/s"])},

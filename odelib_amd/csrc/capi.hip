@@ -271,7 +271,13 @@ int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32
   std::vector<int> cand;
   for (int v = 0; v < kN; ++v)
     if (rk4_variant_ok(e, ia.W, v, nt)) cand.push_back(v);
+  // n back-to-back launches timed after one untimed launch of the same kernel: every timed
+  // launch then follows a launch of its own kind, as in a series (a launch that ends with
+  // part of its output still dirty in the 256 MB MALL pays for it in the next launch, so an
+  // isolated or first-after-idle launch flatters the kernels that leave more dirty lines:
+  // the piped ones)
   auto batch = [&](int v, int n, float* ms) -> int {
+    OE_HIP(c, launch_rk4_traj(c, e, ia, v, nt, flags));
     OE_HIP(c, hipEventRecord(c->ev0, c->stream));
     for (int k = 0; k < n; ++k) OE_HIP(c, launch_rk4_traj(c, e, ia, v, nt, flags));
     OE_HIP(c, hipEventRecord(c->ev1, c->stream));
@@ -284,7 +290,8 @@ int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32
   float ms = 0.f;
   int rc = batch(dflt, 1, &ms);
   if (rc) return rc;
-  const int per = ms > 4.f ? 2 : 8;  // launches per measurement
+  // launches per measurement: ~15 ms of work, 4..16 launches
+  const int per = std::max(4, std::min(16, (int)std::ceil(15.0 / std::max(ms, 1e-3f))));
   for (double settled = ms; settled < 60.0;) {
     rc = batch(dflt, per, &ms);
     if (rc) return rc;

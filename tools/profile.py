@@ -79,7 +79,11 @@ def pmc_counts(out, counters, bench_args, kernel_regex, timeout, base=None, tag=
             key = (r.get("Dispatch_Id"), r.get("Kernel_Name"))
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])  # sum over XCD / instances
         per = list(vals.values())
+        by = {}
+        for (_, name), v in vals.items():
+            by.setdefault(name, []).append(v)
         res[c] = {"dispatches": len(per), "mean": sum(per) / max(len(per), 1), "sum": sum(per),
+                  "by_kernel": {n: {"dispatches": len(v), "mean": sum(v) / len(v)} for n, v in by.items()},
                   "csv": os.path.relpath(path, ROOT)}
     return res
 
@@ -112,20 +116,24 @@ def main():
     for r in stats:
         summary["kernels"].append({k: r[k] for k in r})
     summary["bench_line_under_profiler"] = json.loads(bench_line[-1]) if bench_line else None
-    # the bench's timed region alone: the C1 dispatches after the warmup launches and
-    # before the per-dispatch (event-marked) pass, from the kernel trace
+    # the bench's timed region alone, from the kernel trace: the K dispatches of the kernel
+    # the bench ran (config.kernel; kernel="auto" tunes among several during the warm-up)
+    # right before the K of the per-dispatch (event-marked) pass, which are the last ones
     bl = summary["bench_line_under_profiler"]
     trace_csv = find(os.path.join(d, "**", "*kernel_trace.csv"))
     if bl and trace_csv:
         meth = {"rk4": 0, "dopri5": 1}[bl["config"]["method"]]
-        hot = [r for r in read_csv(trace_csv) if f"k_integrate<oe::TwoI, {meth}, true, true>" in r["Kernel_Name"]]
+        kern = bl["config"].get("kernel", "direct")
+        name = (f"k_integrate_rk4_piped<oe::TwoI, true, {kern[4:]}>" if kern.startswith("pipe")
+                else f"k_integrate<oe::TwoI, {meth}, true, true>")
+        hot = [r for r in read_csv(trace_csv) if name in r["Kernel_Name"]]
         hot.sort(key=lambda r: int(r["Start_Timestamp"]))
-        w, k = bl.get("warmup_launches", bl["warmup"]), bl["steps"]
-        timed = hot[w:w + k]
+        k = bl["steps"]
+        timed = hot[-2 * k:-k]
         if len(timed) == k:
             durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
             span = (int(timed[-1]["End_Timestamp"]) - int(timed[0]["Start_Timestamp"])) / 1e6
-            summary["timed_region"] = {"dispatches": k, "mean_dispatch_ms": sum(durs) / k,
+            summary["timed_region"] = {"kernel": name, "dispatches": k, "mean_dispatch_ms": sum(durs) / k,
                                        "span_ms_per_dispatch": span / k,
                                        "bench_event_kernel_ms": bl["roofline"]["kernel_ms"]}
 
