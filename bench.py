@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--method", default="rk4", choices=["rk4", "dopri5"])
     ap.add_argument("--times", type=int, default=1000)
     ap.add_argument("--cached-stores", action="store_true", help="plain (cached) trajectory stores")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "half", "pipe2", "pipe4", "pipe8"],
+    ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "half", "pipe2", "pipe4", "pipe8", "pipe2x", "pipe4x", "pipe8x"],
                     help="RK4 trajectory kernel: auto = the library times the bitwise-identical kernels on "
                          "this device (OE_TUNE, during the warm-up) and keeps the fastest; or a fixed one (A/B)")
     ap.add_argument("--half-waves", action="store_true", help="same as --kernel half")
@@ -163,7 +163,7 @@ def traffic_of(by_kernel, variant, method):
     if not by_kernel:
         return None
     meth = {"rk4": 0, "dopri5": 1}[method]
-    want = (("k_integrate_rk4_piped<", f", true, {variant[4:]}>") if variant.startswith("pipe")
+    want = (("k_integrate_rk4_piped<", f", true, {variant[4:].rstrip('x')}>") if variant.startswith("pipe")
             else ("k_integrate<", f", {meth}, true, true>"))
     hits = [v["bytes"] for n, v in by_kernel.items() if all(x in n for x in want)]
     return hits[0] if hits else None

@@ -114,7 +114,7 @@ enum {
                            14..22 states: K = 2; 24+ states, a multiple of 4: K = 4).  A split
                            wave holds 64/K walkers, which share one step size, so results differ
                            from the one-lane grouping (64 walkers per step size) within tolerance */
-  OE_TUNE = 8192u       /* oe_integrate, OE_METHOD_RK4 with a trajectory: pick the fastest of the
+  OE_TUNE = 8192u,      /* oe_integrate, OE_METHOD_RK4 with a trajectory: pick the fastest of the
                            RK4 trajectory kernels (OE_KERNEL_*; all produce the same bits) for this
                            shape on this device.  The first call for a shape (model, W, T,
                            substeps, store policy, XCD order) runs each candidate back to back
@@ -122,17 +122,24 @@ enum {
                            and keeps the fastest (the default kernel unless another is > 1 %
                            faster); later calls reuse the choice.  The first call synchronizes
                            the stream.  Overrides OE_PIPE*, OE_HALF_WAVES. */
+  OE_PIPE_XCD = 16384u  /* with OE_PIPE / OE_PIPE_4 / OE_PIPE_8: the piped kernel's workgroups dealt
+                           to the XCDs in runs of 512 walkers (OE_KERNEL_PIPE*X) */
 };
 
-/* RK4 trajectory kernels (oe_last_variant; all bitwise identical) */
+/* RK4 trajectory kernels (oe_last_variant; all bitwise identical; OE_TUNE times those
+ * available for the shape: the piped ones need W even and n_states <= 8, a built-in model,
+ * the X ones the default XCD order) */
 enum {
   OE_KERNEL_DIRECT = 0, /* one walker per lane, 64 walkers per wavefront, stores from the compute waves */
   OE_KERNEL_HALF = 1,   /* 32 walkers per wavefront (OE_HALF_WAVES) */
   OE_KERNEL_PIPE2 = 2,  /* producer/consumer: 4 compute waves + 2 / 4 / 8 store waves per workgroup */
   OE_KERNEL_PIPE4 = 3,  /*   through an LDS ring (OE_PIPE / OE_PIPE_4 / OE_PIPE_8) */
   OE_KERNEL_PIPE8 = 4,
-  OE_KERNEL_OTHER = 5,  /* not an RK4 trajectory launch (DOPRI5, stiff, no trajectory, MH) */
-  OE_KERNEL_COUNT = 6
+  OE_KERNEL_PIPE2X = 5, /* the same with the workgroups dealt to the XCDs in runs of 512 walkers */
+  OE_KERNEL_PIPE4X = 6, /*   (the piped kernels' default is blockIdx order) */
+  OE_KERNEL_PIPE8X = 7,
+  OE_KERNEL_OTHER = 8,  /* not an RK4 trajectory launch (DOPRI5, stiff, no trajectory, MH) */
+  OE_KERNEL_COUNT = 9
 };
 
 /* RNG modes for oe_mh_run */

@@ -234,18 +234,21 @@ int32_t xcd_remap_of(uint32_t flags, const dim3& grid, int64_t per_block) {
 }
 
 // an RK4 trajectory kernel (OE_KERNEL_*) available for this entry and walker count
-bool rk4_variant_ok(const Entry* e, int64_t W, int variant, bool nt) {
+bool rk4_variant_ok(const Entry* e, int64_t W, int variant, bool nt, uint32_t flags) {
   if (variant == OE_KERNEL_DIRECT || variant == OE_KERNEL_HALF) return true;
-  if (variant < OE_KERNEL_PIPE2 || variant > OE_KERNEL_PIPE8) return false;
-  return !e->rtc && W % 2 == 0 && e->rk4_piped[variant - OE_KERNEL_PIPE2][nt ? 1 : 0] != nullptr;
+  if (variant < OE_KERNEL_PIPE2 || variant > OE_KERNEL_PIPE8X) return false;
+  if (variant >= OE_KERNEL_PIPE2X && (flags & (OE_NO_XCD_REMAP | OE_XCD_RANGES))) return false;
+  return !e->rtc && W % 2 == 0 && e->rk4_piped[(variant - OE_KERNEL_PIPE2) % 3][nt ? 1 : 0] != nullptr;
 }
 
 // one RK4 trajectory launch with the given kernel (same bits for every variant)
 hipError_t launch_rk4_traj(oe_ctx* c, const Entry* e, IntegrateArgs ia, int variant, bool nt, uint32_t flags) {
   const int64_t W = ia.W;
   if (variant >= OE_KERNEL_PIPE2) {
-    const int pv = variant - OE_KERNEL_PIPE2;
+    const int pv = (variant - OE_KERNEL_PIPE2) % 3;
     const dim3 grid((unsigned)((W + kPipeWalkers - 1) / kPipeWalkers)), block(256 + 64 * (2 << pv));
+    // blockIdx order, or (X) runs of 512 walkers per XCD as the direct kernel's
+    ia.xcd_remap = variant >= OE_KERNEL_PIPE2X ? (int32_t)(512 / kPipeWalkers) : 0;
     e->rk4_piped[pv][nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
     return hipGetLastError();
   }
@@ -270,7 +273,7 @@ int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32
   constexpr int kN = OE_KERNEL_COUNT - 1;
   std::vector<int> cand;
   for (int v = 0; v < kN; ++v)
-    if (rk4_variant_ok(e, ia.W, v, nt)) cand.push_back(v);
+    if (rk4_variant_ok(e, ia.W, v, nt, flags)) cand.push_back(v);
   // n back-to-back launches timed after one untimed launch of the same kernel: every timed
   // launch then follows a launch of its own kind, as in a series (a launch that ends with
   // part of its output still dirty in the 256 MB MALL pays for it in the next launch, so an
@@ -638,9 +641,10 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   if (rk4_traj) {
     const bool auto_half = S >= 5 && W <= (int64_t)64 * 4 * c->n_cu;
     const int dflt = ((flags & OE_HALF_WAVES) || auto_half) ? OE_KERNEL_HALF : OE_KERNEL_DIRECT;
-    const int asked = (flags & OE_PIPE_8) ? OE_KERNEL_PIPE8 : (flags & OE_PIPE_4) ? OE_KERNEL_PIPE4
-                      : (flags & OE_PIPE) ? OE_KERNEL_PIPE2 : dflt;
-    variant = rk4_variant_ok(e, W, asked, nt) ? asked : dflt;
+    const int xcd = (flags & OE_PIPE_XCD) ? OE_KERNEL_PIPE2X - OE_KERNEL_PIPE2 : 0;
+    const int asked = (flags & OE_PIPE_8) ? OE_KERNEL_PIPE8 + xcd : (flags & OE_PIPE_4) ? OE_KERNEL_PIPE4 + xcd
+                      : (flags & OE_PIPE) ? OE_KERNEL_PIPE2 + xcd : dflt;
+    variant = rk4_variant_ok(e, W, asked, nt, flags) ? asked : dflt;
     if (flags & OE_TUNE) {
       int idx = -1;
       rc = tune_rk4(c, e, ia, nt, flags, dflt, &idx);

@@ -933,7 +933,10 @@ __global__ void __launch_bounds__(256)
 // vmcnt.  Same arithmetic, same outputs as k_integrate<M, RK4, true, NT>.
 // ---------------------------------------------------------------------------------
 constexpr int kPipeWalkers = 256;  // walkers per workgroup (4 compute waves)
-constexpr int kPipeLdsBytes = 128 * 1024;
+#ifndef OE_PIPE_LDS_BYTES
+#define OE_PIPE_LDS_BYTES (160 * 1024)  // all of a CU's LDS: one workgroup per CU either way
+#endif
+constexpr int kPipeLdsBytes = OE_PIPE_LDS_BYTES;
 
 template <int S>
 constexpr int pipe_rows() { return (kPipeLdsBytes / (2 * S * kPipeWalkers * 8)) > 0 ? (kPipeLdsBytes / (2 * S * kPipeWalkers * 8)) : 1; }
@@ -958,9 +961,10 @@ __global__ void __launch_bounds__(256 + 64 * NSW) k_integrate_rk4_piped(const De
   const int T = pb.T;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  // blockIdx order (the XCD-contiguous remap of the direct kernel measured 9 % slower here:
-  // 0.400 vs 0.366 ms on C1, profiles/r02l_time_modes.log)
-  const int64_t base = (int64_t)blockIdx.x * kPipeWalkers;
+  // blockIdx order by default (the XCD-contiguous remap of the direct kernel measured 9 %
+  // slower here: 0.400 vs 0.366 ms on C1, profiles/r02l_time_modes.log)
+  const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x, ia.xcd_remap) : (int64_t)blockIdx.x;
+  const int64_t base = blk * kPipeWalkers;
   const int nphase = (T + H - 1) / H;
 
   if (wave < 4) {

@@ -261,15 +261,15 @@ class Engine:
         otherwise spreads a walker over 2 or 4 lanes (OE_NO_SPLIT; the wide built-in chain).
         ``kernel`` names the RK4 trajectory kernel instead: "direct" (the library's default
         rule: 32 walkers per wave for 5+ states at <= 1 wave per SIMD), "half", "pipe2",
-        "pipe4", "pipe8", or "auto" (OE_TUNE: the library measures the available ones for
+        "pipe4", "pipe8" (blockIdx order), "pipe2x", "pipe4x", "pipe8x" (XCD runs), or "auto" (OE_TUNE: the library measures the available ones for
         this shape on the first call and keeps the fastest; ``last_variant()`` says which
         ran).  All of them produce the same bits."""
         torch = self.torch
         if kernel is not None:
-            if kernel not in ("auto", "direct", "half", "pipe2", "pipe4", "pipe8"):
+            if kernel not in ("auto",) + N.KERNEL_NAMES[:-1]:
                 raise ValueError(f"unknown kernel {kernel!r}")
             if kernel != "auto":
-                pipelined = {"direct": False, "half": False, "pipe2": 2, "pipe4": 4, "pipe8": 8}[kernel]
+                pipelined = {"direct": False, "half": False, "pipe2": 2, "pipe4": 4, "pipe8": 8}[kernel.rstrip("x")]
                 half_waves = (kernel == "half")
         pb = self.problem
         theta_t = theta if isinstance(theta, torch.Tensor) else np.asarray(theta)
@@ -291,7 +291,8 @@ class Engine:
             | (N.OE_HALF_WAVES if half_waves else 0) \
             | (N.OE_XCD_RANGES if xcd_remap == "ranges" else 0 if xcd_remap else N.OE_NO_XCD_REMAP) \
             | (0 if timing else N.OE_NO_TIMING) | (0 if split else N.OE_NO_SPLIT) \
-            | (N.OE_TUNE if kernel == "auto" else 0)
+            | (N.OE_TUNE if kernel == "auto" else 0) \
+            | (N.OE_PIPE_XCD if kernel is not None and kernel.endswith("x") else 0)
         self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)
         if sync:
             torch.cuda.synchronize(self.dev)
@@ -302,7 +303,8 @@ class Engine:
 
     def last_variant(self) -> str:
         """Name of the kernel the last ``integrate`` launched ("direct", "half", "pipe2",
-        "pipe4", "pipe8"; "other" for DOPRI5, the stiff methods, no trajectory)."""
+        "pipe4", "pipe8", "pipe2x", "pipe4x", "pipe8x"; "other" for DOPRI5, the stiff
+        methods, no trajectory)."""
         return N.KERNEL_NAMES[self.ctx.last_variant()]
 
     def tune_times(self) -> dict:

@@ -99,9 +99,13 @@ def test_rk4_tuned_kernel_choice(spec, W):
     chosen = eng.last_variant()
     assert chosen in tuned and set(tuned) >= {"direct", "half"}
     assert all(0 < v < 1e3 for v in tuned.values()), tuned
-    piped = {"pipe2", "pipe4", "pipe8"} & set(tuned)
-    assert piped == (set() if (W % 2 or int(spec[5:] if spec.startswith("chain") else 4) > 8)
-                     else {"pipe2", "pipe4", "pipe8"})
+    piped = {"pipe2", "pipe4", "pipe8", "pipe2x", "pipe4x", "pipe8x"}
+    assert piped & set(tuned) == (set() if (W % 2 or int(spec[5:] if spec.startswith("chain") else 4) > 8)
+                                  else piped)
+    for k in sorted(piped & set(tuned)):  # each piped kernel by name, incl. the XCD-ordered ones
+        d = eng.integrate(y0, theta, kernel=k)
+        assert eng.last_variant() == k
+        assert np.array_equal(d["traj"].cpu().numpy(), b["traj"].cpu().numpy()), k
     for key in ("traj", "chi", "ssres", "status"):
         assert np.array_equal(a[key].cpu().numpy(), b[key].cpu().numpy(), equal_nan=True), key
     c = eng.integrate(y0, theta, kernel="auto")  # cached: same choice, same numbers reported

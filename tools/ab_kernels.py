@@ -13,7 +13,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KERNELS = ("direct", "half", "pipe2", "pipe4", "pipe8")
+KERNELS = ("direct", "half", "pipe2", "pipe4", "pipe8", "pipe2x", "pipe4x", "pipe8x")
 
 
 def main():

@@ -124,7 +124,7 @@ def main():
     if bl and trace_csv:
         meth = {"rk4": 0, "dopri5": 1}[bl["config"]["method"]]
         kern = bl["config"].get("kernel", "direct")
-        name = (f"k_integrate_rk4_piped<oe::TwoI, true, {kern[4:]}>" if kern.startswith("pipe")
+        name = (f"k_integrate_rk4_piped<oe::TwoI, true, {kern[4:].rstrip('x')}>" if kern.startswith("pipe")
                 else f"k_integrate<oe::TwoI, {meth}, true, true>")
         hot = [r for r in read_csv(trace_csv) if name in r["Kernel_Name"]]
         hot.sort(key=lambda r: int(r["Start_Timestamp"]))
