@@ -94,7 +94,7 @@ enum {
   OE_HOST_PTRS = 1u, /* buffers are host memory */
   OE_ASYNC = 2u,     /* do not synchronize before returning (device pointers only) */
   OE_NT_STORES = 4u, /* non-temporal trajectory stores */
-  OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel, 2 store waves (S <= 8, W even) */
+  OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel, 2 store waves (built-in models, W even) */
   OE_HALF_WAVES = 16u, /* RK4: 32 walkers per wavefront (twice the waves; same results). Chosen
                          automatically for trajectories with S >= 5 at <= 1 wave per SIMD. */
   /* 32u: reserved (was an experimental split-wave layout, measured slower and removed) */
@@ -127,7 +127,7 @@ enum {
 };
 
 /* RK4 trajectory kernels (oe_last_variant; all bitwise identical; OE_TUNE times those
- * available for the shape: the piped ones need W even and n_states <= 8, a built-in model,
+ * available for the shape: the piped ones need W even and a built-in model,
  * the X ones the default XCD order) */
 enum {
   OE_KERNEL_DIRECT = 0, /* one walker per lane, 64 walkers per wavefront, stores from the compute waves */

@@ -8,6 +8,11 @@
 
 namespace oe {
 
+// widest model with the producer/consumer RK4 trajectory kernels
+#ifndef OE_PIPE_MAX_S
+#define OE_PIPE_MAX_S 32  // every built-in (A/B: the piped XCD-ordered kernels win up to chain20)
+#endif
+
 // ---- dispatch table ---------------------------------------------------------
 using IntegrateLaunch = void (*)(const DevProblem&, const IntegrateArgs&, dim3, dim3, hipStream_t);
 using MHLaunch = void (*)(const DevProblem&, const MHArgs&, dim3, dim3, hipStream_t);
@@ -19,7 +24,7 @@ struct Entry {
   int32_t P;  // the model's own parameter count
   // [method][traj][nt]; methods kAuto / kRosenbrock are null when S > kStiffMaxS
   IntegrateLaunch integrate[4][2][2];
-  IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > 8
+  IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > OE_PIPE_MAX_S
   MHLaunch mh[4];
   StiffWaveLaunch stiff_wave[2][2];  // [traj][nt]: S > kStiffRegS stiff redo, one wave per walker
   IntegrateLaunch dopri5_split[2][2];  // [traj][nt]: DOPRI5 with split_lanes lanes per walker (split.cuh)
@@ -134,7 +139,7 @@ Entry make_entry(int32_t model_id) {
     e.dopri5_split[1][1] = launch_split<M::S, K, true, true>;
     e.mh_split = launch_mh_split<M::S, K>;
   }
-  if constexpr (M::S <= 8) {
+  if constexpr (M::S <= OE_PIPE_MAX_S) {
     e.rk4_piped[0][0] = launch_rk4_piped<M, false, 2>;
     e.rk4_piped[0][1] = launch_rk4_piped<M, true, 2>;
     e.rk4_piped[1][0] = launch_rk4_piped<M, false, 4>;

@@ -920,7 +920,7 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------------------------
-// Kernel 1b: RK4 trajectory mode with producer/consumer waves (S <= 8, W even).
+// Kernel 1b: RK4 trajectory mode with producer/consumer waves (W even).
 //
 // One workgroup = 4 COMPUTE waves (256 walkers, one per lane) + NSW STORE waves (2, 4
 // or 8).  Output rows are produced in phases of H rows into one half of a

@@ -63,7 +63,7 @@ def test_rk4_bitwise_vs_c_restatement(spec, W):
     assert np.array_equal(out["status"], ref["status"])
 
 
-@pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain5", "chain8"])
+@pytest.mark.parametrize("spec", ["zero_i", "one_i", "two_i", "chain5", "chain8", "chain12", "chain20", "chain32"])
 @pytest.mark.parametrize("W", [2, 258, 4098])
 def test_rk4_pipelined_kernel_matches_direct_kernel(spec, W):
     """The producer/consumer trajectory kernel (4 compute + 2 store waves, LDS ring)
@@ -87,7 +87,7 @@ def test_rk4_pipelined_kernel_matches_direct_kernel(spec, W):
 def test_rk4_tuned_kernel_choice(spec, W):
     """kernel="auto" (OE_TUNE): the library times the available RK4 trajectory kernels for
     the shape, keeps the fastest, reuses the choice, and the result is the bits of the
-    default kernel and of the C restatement.  Odd W and S > 8 have no piped kernel."""
+    default kernel and of the C restatement.  Odd W has no piped kernel."""
     m = _model(spec, "rk4")
     theta = _walkers(spec, W)
     y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
@@ -100,8 +100,7 @@ def test_rk4_tuned_kernel_choice(spec, W):
     assert chosen in tuned and set(tuned) >= {"direct", "half"}
     assert all(0 < v < 1e3 for v in tuned.values()), tuned
     piped = {"pipe2", "pipe4", "pipe8", "pipe2x", "pipe4x", "pipe8x"}
-    assert piped & set(tuned) == (set() if (W % 2 or int(spec[5:] if spec.startswith("chain") else 4) > 8)
-                                  else piped)
+    assert piped & set(tuned) == (set() if W % 2 else piped)
     for k in sorted(piped & set(tuned)):  # each piped kernel by name, incl. the XCD-ordered ones
         d = eng.integrate(y0, theta, kernel=k)
         assert eng.last_variant() == k
