@@ -211,6 +211,17 @@ typedef struct {
                                  max(k, burnin+1)..nits-1.  Philox counters and replay arrays
                                  are indexed by iteration; NUMPY streams are re-seeded and
                                  fast-forwarded on the device.  Same results as one run. */
+  int32_t speculate;          /* (ABI 5) speculative rounds for small ensembles: 0 = off (one
+                                 iteration per step), -1 = depth chosen by the library (off when
+                                 the chains fill the device), d >= 2: d iterations per round.  A
+                                 round integrates every proposal the next d accept/reject
+                                 decisions can lead to (2^d - 1 per chain) at once, then keeps
+                                 each chain's actual path: the same Markov chain, the same draws
+                                 in the same order.  RK4: bitwise the chains of speculate = 0;
+                                 DOPRI5 / auto: within the integration tolerance (a wave's 64
+                                 lanes share one step size, and they are other proposals here).
+                                 One-lane MH kernels of the built-in models only (ignored for the
+                                 split DOPRI5 kernels and hipRTC models). */
 } oe_mh_args;
 
 int oe_abi_version(void);
@@ -290,6 +301,9 @@ int oe_allgather_samples(oe_comm* comm, int64_t rows, const double* block, const
  * from HIP events recorded on the context's stream around them (waits for them). */
 int oe_last_kernel_ms(oe_ctx* ctx, double* ms);
 
+/* Iterations per speculative round of the last oe_mh_run (oe_mh_args.speculate); 0 = it ran
+ * one iteration per step. */
+int oe_last_mh_depth(oe_ctx* ctx, int32_t* depth);
 /* The kernel (OE_KERNEL_*) the last oe_integrate launched.  OE_ERR_STATE before any call. */
 int oe_last_variant(oe_ctx* ctx, int32_t* variant);
 /* OE_TUNE's measurements for the shape of the last oe_integrate: ms[k] = mean launch time of

@@ -55,6 +55,7 @@ EXPORTED = (
     "oe_allgather_samples",
     "oe_last_variant",
     "oe_tune_times",
+    "oe_last_mh_depth",
 )
 
 
@@ -112,6 +113,7 @@ class OEMHArgs(C.Structure):
         ("numpy_seeds", C.c_void_p),
         ("numpy_prior_draws", C.c_int32),
         ("it_start", C.c_int32),
+        ("speculate", C.c_int32),
     ]
 
 
@@ -180,6 +182,8 @@ def load_library(path: str | None = None):
         lib.oe_allgather_samples.argtypes = [vp, i64, vp, vp, vp, u32]
         lib.oe_last_variant.restype = C.c_int
         lib.oe_last_variant.argtypes = [vp, C.POINTER(i32)]
+        lib.oe_last_mh_depth.restype = C.c_int
+        lib.oe_last_mh_depth.argtypes = [vp, C.POINTER(i32)]
         lib.oe_tune_times.restype = C.c_int
         lib.oe_tune_times.argtypes = [vp, C.POINTER(C.c_double), i32]
         if lib.oe_abi_version() != OE_ABI_VERSION:
@@ -264,6 +268,12 @@ class Context:
         """OE_KERNEL_* of the last oe_integrate."""
         v = C.c_int32(-1)
         self._check(self.lib.oe_last_variant(self._h, C.byref(v)), "oe_last_variant")
+        return v.value
+
+    def last_mh_depth(self) -> int:
+        """Iterations per speculative round of the last oe_mh_run (0: sequential)."""
+        v = C.c_int32(0)
+        self._check(self.lib.oe_last_mh_depth(self._h, C.byref(v)), "oe_last_mh_depth")
         return v.value
 
     def tune_times(self) -> dict:

@@ -97,6 +97,9 @@ struct oe_ctx {
   size_t np_state_bytes = 0;
   int32_t* stiff_buf = nullptr;  // wide-model stiff redo: [count][list W][status W]
   size_t stiff_cap = 0;          // walkers it holds
+  void* tree = nullptr;          // speculative MH rounds: node proposals and results
+  size_t tree_bytes = 0;
+  int32_t last_mh_depth = 0;     // iterations per round of the last oe_mh_run (0: sequential)
   // OE_TUNE: the RK4 trajectory kernel chosen per shape, with what was measured
   struct Tuned {
     const Entry* e;
@@ -339,6 +342,63 @@ __global__ void __launch_bounds__(256) k_philox_draws(const oe::DrawArgs d) {
   if (w < d.W) oe::philox_draws(d, w);
 }
 
+// k_mh_tree's resolution: one lane per chain walks its tree with k_mh's accept test and
+// bookkeeping, iteration by iteration, in the reference's arithmetic (Samplers.py:124-153)
+__global__ void __launch_bounds__(256) k_mh_resolve(const oe::DevProblem pb, const oe::MHTreeArgs ta, int32_t S) {
+  using namespace oe;
+  const MHArgs& ma = ta.m;
+  const int64_t W = ma.W;
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  const int P = pb.P;
+  const int PS = P + 5;
+  const uint32_t off = (uint32_t)w * 8u;
+  double* cur = ma.cur;
+  double chi = Row(cur, W).ld(off), rsq = Row(cur + W, W).ld(off), aic = Row(cur + 2 * W, W).ld(off);
+  double nacc = Row(cur + 3 * W, W).ld(off);
+  uint32_t path = 0;
+  for (int j = 0; j < ta.depth; ++j) {
+    const int it = ma.it0 + j;
+    const int64_t n = (int64_t)(1u << j) - 1 + path;
+    const double chin = ta.node_chi[n * W + w];
+    const double u = Row(ma.u + (int64_t)(it - ma.draw_it0) * W, W).ld(off);
+    const double lr = oe_exp(chi - chin);
+    const double accp = oe_exp(oe_log(lr));
+    const bool acc = accp > u;
+    // the parameters after this iteration: the proposal if accepted, else the chain's
+    // (read from the node, resp. from θ before anything of this iteration is stored)
+    const double* src = acc ? ta.node_th + n * P * W : ma.theta;
+    if (acc) {
+      chi = chin;
+      rsq = 1.0 - ta.node_ss[n * W + w] / pb.sstot;
+      aic = -2.0 * (-chi) + 2.0 * (double)pb.pnum;
+      nacc += 1.0;
+      for (int q = 0; q < P; ++q) Row(ma.theta + (int64_t)q * W, W).st(off, Row(src + (int64_t)q * W, W).ld(off));
+      if (ma.status) ma.status[w] = ta.node_st[n * W + w];
+    }
+    if (ma.any_walk) {
+      for (int s = 0; s < S; ++s) {
+        const int pi = ma.init_param[s];
+        if (pi >= 0) Row(ma.y0 + (int64_t)s * W, W).st(off, Row(src + (int64_t)pi * W, W).ld(off));
+      }
+    }
+    if (it > ma.burnin) {
+      double* row = ma.samples + (int64_t)(it - ma.row0) * PS * W;
+      for (int q = 0; q < P; ++q) Row(row + (int64_t)q * W, W).st(off, Row(src + (int64_t)q * W, W).ld(off));
+      Row(row + (int64_t)P * W, W).st(off, chi);
+      Row(row + (int64_t)(P + 1) * W, W).st(off, rsq);
+      Row(row + (int64_t)(P + 2) * W, W).st(off, aic);
+      Row(row + (int64_t)(P + 3) * W, W).st(off, (double)it);
+      Row(row + (int64_t)(P + 4) * W, W).st(off, nacc / (double)it);
+    }
+    path |= (acc ? 1u : 0u) << j;
+  }
+  Row(cur, W).st(off, chi);
+  Row(cur + W, W).st(off, rsq);
+  Row(cur + 2 * W, W).st(off, aic);
+  Row(cur + 3 * W, W).st(off, nacc);
+}
+
 extern "C" {
 
 int oe_abi_version(void) { return OE_ABI_VERSION; }
@@ -399,6 +459,7 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->draws) (void)hipFree(c->draws);
     if (c->np_state) (void)hipFree(c->np_state);
     if (c->stiff_buf) (void)hipFree(c->stiff_buf);
+    if (c->tree) (void)hipFree(c->tree);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (auto& m : c->custom)
@@ -803,6 +864,42 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
     return launch_mh_entry(e, c->method, c->dp, args, grid, block, c->stream);
   };
   int chunk = a->chunk > 0 ? a->chunk : 25;
+  // Speculative rounds (k_mh_tree + k_mh_resolve): d iterations per round, the tree's
+  // (2^d - 1)·W lanes at most about one wave per SIMD, so a round costs about what one
+  // iteration of the few chains costs alone
+  int depth = 0;
+  if (a->speculate != 0 && !split && !e->rtc && e->mh_tree[c->method] && a->nits > 1) {
+    const int64_t target = (int64_t)64 * 4 * c->n_cu;
+    if (a->speculate < 0) {
+      depth = 1;
+      while (depth < 16 && ((int64_t(1) << (depth + 1)) - 1) * W <= target) ++depth;
+    } else {
+      depth = std::min(a->speculate, 16);
+    }
+    if (depth < 2 || ((int64_t(1) << depth) - 1) * W > kMaxWalkers) depth = 0;
+  }
+  c->last_mh_depth = depth;
+  MHTreeArgs ta{};
+  if (depth) {
+    chunk = std::max(depth, chunk / depth * depth);  // whole rounds per chunk of draws
+    const int64_t nodes = (int64_t(1) << depth) - 1;
+    const size_t bytes = sizeof(double) * (size_t)(nodes * W) * (size_t)(P + 2) + sizeof(int32_t) * (size_t)(nodes * W) + 256;
+    if (c->tree_bytes < bytes) {
+      if (c->tree) {
+        OE_HIP(c, hipStreamSynchronize(c->stream));
+        OE_HIP(c, hipFree(c->tree));
+        c->tree = nullptr;
+        c->tree_bytes = 0;
+      }
+      OE_HIP(c, hipMalloc(&c->tree, bytes));
+      c->tree_bytes = bytes;
+    }
+    double* b = static_cast<double*>(c->tree);
+    ta.node_th = b;
+    ta.node_chi = b + (size_t)(nodes * W) * P;
+    ta.node_ss = ta.node_chi + nodes * W;
+    ta.node_st = reinterpret_cast<int32_t*>(ta.node_ss + nodes * W);
+  }
   const bool philox = a->rng_mode == OE_RNG_PHILOX, numpy = a->rng_mode == OE_RNG_NUMPY;
   DrawArgs d{};
   NpDrawArgs nd{};
@@ -876,7 +973,21 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       hipLaunchKernelGGL(k_np_draws, grid, block, 0, c->stream, nd);
       OE_HIP(c, hipGetLastError());
     }
-    OE_HIP(c, launch_mh(m));
+    if (!depth) {
+      OE_HIP(c, launch_mh(m));
+      continue;
+    }
+    for (int r0 = m.it0; r0 < m.it1; r0 += ta.depth) {
+      ta.m = m;
+      ta.m.it0 = r0;
+      ta.depth = std::min(depth, m.it1 - r0);
+      ta.n_lanes = ((int64_t(1) << ta.depth) - 1) * W;
+      const dim3 tgrid((unsigned)((ta.n_lanes + kBlock - 1) / kBlock));
+      e->mh_tree[c->method](c->dp, ta, tgrid, block, c->stream);
+      OE_HIP(c, hipGetLastError());
+      hipLaunchKernelGGL(k_mh_resolve, grid, block, 0, c->stream, c->dp, ta, (int32_t)S);
+      OE_HIP(c, hipGetLastError());
+    }
   }
   OE_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
@@ -935,6 +1046,12 @@ int oe_last_variant(oe_ctx* c, int32_t* variant) {
   if (!c || !variant) return OE_ERR_ARG;
   if (c->last_variant < 0) return fail(c, OE_ERR_STATE, "oe_last_variant: no oe_integrate yet");
   *variant = c->last_variant;
+  return OE_OK;
+}
+
+int oe_last_mh_depth(oe_ctx* c, int32_t* depth) {
+  if (!c || !depth) return OE_ERR_ARG;
+  *depth = c->last_mh_depth;
   return OE_OK;
 }
 

@@ -17,6 +17,7 @@ namespace oe {
 using IntegrateLaunch = void (*)(const DevProblem&, const IntegrateArgs&, dim3, dim3, hipStream_t);
 using MHLaunch = void (*)(const DevProblem&, const MHArgs&, dim3, dim3, hipStream_t);
 using StiffWaveLaunch = void (*)(const DevProblem&, const StiffWaveArgs&, dim3, dim3, hipStream_t);
+using MHTreeLaunch = void (*)(const DevProblem&, const MHTreeArgs&, dim3, dim3, hipStream_t);
 
 struct Entry {
   int32_t model_id;
@@ -26,6 +27,7 @@ struct Entry {
   IntegrateLaunch integrate[4][2][2];
   IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > OE_PIPE_MAX_S
   MHLaunch mh[4];
+  MHTreeLaunch mh_tree[4];  // speculative MH rounds (k_mh_tree); the resolve kernel is shared
   StiffWaveLaunch stiff_wave[2][2];  // [traj][nt]: S > kStiffRegS stiff redo, one wave per walker
   IntegrateLaunch dopri5_split[2][2];  // [traj][nt]: DOPRI5 with split_lanes lanes per walker (split.cuh)
   MHLaunch mh_split = nullptr;         // DOPRI5 Metropolis–Hastings, split_lanes lanes per walker
@@ -69,6 +71,10 @@ template <class M, int METHOD>
 void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_mh<M, METHOD>), g, b, 0, s, pb, ma);
 }
+template <class M, int METHOD>
+void launch_mh_tree(const DevProblem& pb, const MHTreeArgs& ta, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_mh_tree<M, METHOD>), g, b, 0, s, pb, ta);
+}
 template <class M, bool TRAJ, bool NT>
 void launch_stiff_wave(const DevProblem& pb, const StiffWaveArgs& sa, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_stiff_wave<M, TRAJ, NT>), g, b, 0, s, pb, sa);
@@ -110,6 +116,7 @@ void fill_method(Entry& e) {
   e.integrate[METHOD][1][0] = launch_integrate<M, METHOD, true, false>;
   e.integrate[METHOD][1][1] = launch_integrate<M, METHOD, true, true>;
   e.mh[METHOD] = launch_mh<M, METHOD>;
+  e.mh_tree[METHOD] = launch_mh_tree<M, METHOD>;
 }
 
 template <class M>

@@ -1324,6 +1324,91 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Kernel 2b: speculative Metropolis–Hastings for small ensembles (prefetching MH).
+// A chain's proposal at iteration it depends on the chain state, i.e. on which of the
+// earlier proposals were accepted, but its draws (dz[it], u[it]) do not.  One round
+// covers iterations it0 .. it0+d-1: every outcome path of the first j accept/reject
+// decisions gives one candidate state for iteration it0+j, so the 2^d - 1 nodes of the
+// binary tree hold every proposal the chain can make in the round.  k_mh_tree integrates
+// all of them at once (one lane per (node, chain)); k_mh_resolve then walks each chain's
+// tree with the accept test and keeps the path the sequential chain takes.  Each node's
+// proposal is formed by the same operations, in the same order, as k_mh forms it on that
+// path (θ ← exp(log θ + dz) per accepted iteration), and RK4 integrates a lane on its own,
+// so RK4 chains are bitwise those of k_mh; a DOPRI5 lane shares its step size with the 63
+// lanes of its wave, which are other nodes here, so DOPRI5 chains agree within the
+// integration tolerance.  For W chains the round keeps (2^d - 1)·W lanes busy: with few
+// chains the GPU is mostly idle in k_mh, and d iterations cost about one.
+// Node n (heap order): depth j = floor(log2(n + 1)), path bits p = n + 1 - 2^j, bit k of p
+// = the decision at depth k; lane layout node-major, [n][W].
+// ---------------------------------------------------------------------------------
+struct MHTreeArgs {
+  MHArgs m;            // chain state, draws, masks; m.it0 = the round's first iteration
+  int32_t depth;       // iterations of this round (the tree has 2^depth - 1 nodes)
+  int64_t n_lanes;     // (2^depth - 1) * W
+  double* node_th;     // [n][P][W] proposals
+  double* node_chi;    // [n][W] chi of the proposal (NaN if no observation was finite)
+  double* node_ss;     // [n][W] R² residual
+  int32_t* node_st;    // [n][W] status bits
+};
+
+template <class M, int METHOD>
+__global__ void __launch_bounds__(256)
+    __attribute__((amdgpu_waves_per_eu((METHOD >= kAuto && M::S == 5) ? 2 : 1)))
+    k_mh_tree(const DevProblem pb, const MHTreeArgs ta) {
+  constexpr int S = M::S;
+  constexpr int PMAX = kPmax<M>;
+  const MHArgs& ma = ta.m;
+  const int64_t W = ma.W;
+  const int P = pb.P;
+  const int64_t gl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = gl < ta.n_lanes;
+  const int64_t g = active ? gl : ta.n_lanes - 1;
+  const int64_t n = g / W;
+  const int64_t c = g - n * W;
+  const int j = 31 - __builtin_clz((uint32_t)(n + 1));  // depth
+  const uint32_t path = (uint32_t)(n + 1) - (1u << j);
+  const uint32_t off = (uint32_t)c * 8u;
+  // the chain state this path reaches at depth j: the round's start, moved on by every
+  // accepted proposal of the path, each formed as k_mh forms it
+  double th[PMAX];
+#pragma unroll
+  for (int q = 0; q < PMAX; ++q) th[q] = (q < P) ? Row(ma.theta + (int64_t)q * W, W).ld(off) : 0.0;
+  for (int k = 0; k < j; ++k) {
+    if (!((path >> k) & 1u)) continue;
+    const double* dz = ma.dz + (int64_t)(ma.it0 + k - ma.draw_it0) * P * W;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q)
+      if (q < P && ((ma.walk_mask >> q) & 1ull)) th[q] = oe_exp(oe_log(th[q]) + Row(dz + (int64_t)q * W, W).ld(off));
+  }
+  double tn[PMAX];
+  {
+    const double* dz = ma.dz + (int64_t)(ma.it0 + j - ma.draw_it0) * P * W;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q)
+      tn[q] = (q < P && ((ma.walk_mask >> q) & 1ull)) ? oe_exp(oe_log(th[q]) + Row(dz + (int64_t)q * W, W).ld(off))
+                                                      : th[q];
+  }
+  double y[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int pi = ma.init_param[s];
+    y[s] = (ma.any_walk && pi >= 0) ? pick(tn, pi) : Row(ma.y0 + (int64_t)s * W, W).ld(off);
+  }
+  Acc a = acc_init();
+  integrate_walker<M, PMAX, METHOD, false, false>(pb, y, tn, nullptr, ta.n_lanes, g, active, a);
+  if (active) {
+    const int64_t NW = ta.n_lanes;
+    const uint32_t o = (uint32_t)g * 8u;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q)
+      if (q < P) Row(ta.node_th + n * P * W + (int64_t)q * W, W).st(off, tn[q]);
+    Row(ta.node_chi, NW).st(o, a.nvalid ? a.chi : __builtin_nan(""));
+    Row(ta.node_ss, NW).st(o, a.ssres);
+    ta.node_st[g] = finish(a);
+  }
+}
+
 }  // namespace oe
 #include "stiff_wave.cuh"
 #include "split.cuh"

@@ -307,6 +307,10 @@ class Engine:
         methods, no trajectory)."""
         return N.KERNEL_NAMES[self.ctx.last_variant()]
 
+    def last_mh_depth(self) -> int:
+        """Iterations per speculative round of the last ``mh_run`` (0: one per step)."""
+        return self.ctx.last_mh_depth()
+
     def tune_times(self) -> dict:
         """What ``kernel="auto"`` measured for the last ``integrate``'s shape: ms per kernel."""
         return self.ctx.tune_times()
@@ -333,7 +337,7 @@ class Engine:
     def mh_run(self, theta, y0, nits: int, burnin: int, walk_mask, init_param=None, rng: str = "philox",
                seed: int = 0, replay=None, step_sd: float = 0.05, walker_offset: int = 0, chunk: int = 0,
                sync: bool = True, numpy_seeds=None, prior_draws: int = 0, resume=None,
-               allow_unverified: bool = False, split: bool = True):
+               allow_unverified: bool = False, split: bool = True, speculate=0):
         """Run W chains; returns dict(samples [kept][P+5][W], theta, y0, final [4][W], status).
 
         rng='replay' takes ``replay=(dz [nits-1][P][W], u [nits-1][W])`` (e.g. from
@@ -349,7 +353,13 @@ class Engine:
         holds the kept rows from max(next_it, burnin+1) on.  ``allow_unverified`` resumes a
         checkpoint that predates the random-stream record (see ``check_resume``).
         ``split=False``: one lane per chain for the models whose DOPRI5 MH kernel otherwise
-        spreads a chain over 2 or 4 lanes (OE_NO_SPLIT)."""
+        spreads a chain over 2 or 4 lanes (OE_NO_SPLIT).
+        ``speculate``: speculative rounds for small ensembles (oe_mh_args.speculate): 0 off,
+        "auto" (or -1) the library's depth (off when the chains fill the device), d >= 2
+        iterations per round — every proposal the next d decisions can lead to is integrated
+        at once and each chain keeps its own path: RK4 chains are bitwise those of
+        ``speculate=0``, DOPRI5/auto within the integration tolerance.  ``last_mh_depth()``
+        reports the depth used."""
         torch = self.torch
         pb = self.problem
         P, S = pb.n_params, pb.n_states
@@ -389,6 +399,7 @@ class Engine:
         a.step_sd = float(step_sd)
         a.walk_mask = wm.ctypes.data
         a.init_param = ip.ctypes.data
+        a.speculate = -1 if speculate in ("auto", True) else int(speculate or 0)
         keep = []
         if rng == "replay":
             if replay is None:

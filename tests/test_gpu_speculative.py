@@ -1,0 +1,142 @@
+"""Speculative Metropolis–Hastings rounds (oe_mh_args.speculate; k_mh_tree + k_mh_resolve)
+against the one-iteration-per-step MH kernel, the C restatement and themselves.
+
+The chain a round keeps is the sequential chain: same draws, same proposals (formed by the
+same operations on the same path), same accept test.  RK4 integrates a lane on its own, so
+RK4 chains must be bitwise those of speculate=0; DOPRI5 lanes share a step size with their
+wave, which holds other proposals in a round, so DOPRI5/auto chains take the same
+decisions — hence bitwise the same parameters — with chi, R², AIC within the integration
+tolerance (rtol 1e-7 written below).
+"""
+import numpy as np
+import pytest
+
+from helpers import product_model
+from oracle import rk_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(spec, W, method="rk4", extra=None, seed=9):
+    m = product_model(spec, method=method, extra_params=extra) if extra else product_model(spec, method=method)
+    P = len(m.get_pnames())
+    theta = np.repeat(np.array([float(m.parameters[p].val) for p in m.get_pnames()])[:, None], W, axis=1)
+    theta = theta * np.exp(0.02 * np.random.RandomState(seed).standard_normal(theta.shape))
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    return m, P, theta, y0
+
+
+def _np(r):
+    return {k: r[k].cpu().numpy() for k in ("samples", "theta", "y0", "final", "status")}
+
+
+def _equal(a, b):
+    for k in a:
+        assert np.array_equal(a[k], b[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("W", [1, 5, 70])
+@pytest.mark.parametrize("depth", [2, 3, "auto"])
+@pytest.mark.parametrize("rng", ["philox", "replay", "numpy"])
+def test_rk4_speculative_chains_are_the_sequential_chains(W, depth, rng):
+    """two_i RK4, one static parameter: every output bitwise equal to speculate=0, for
+    fixed and library-chosen depths, a chunk that is not a multiple of the depth, and all
+    three RNG modes (the draws do not depend on the chain state, so a round may consume
+    them ahead)."""
+    m, P, theta, y0 = _inputs("two_i", W)
+    walk = np.ones(P, np.uint8)
+    walk[2] = 0
+    nits, burnin = 31, 9
+    kw = dict(nits=nits, burnin=burnin, walk_mask=walk, chunk=7)
+    if rng == "philox":
+        kw.update(rng="philox", seed=5, walker_offset=3)
+    elif rng == "replay":
+        rs = np.random.RandomState(4)
+        kw.update(rng="replay", replay=(0.05 * rs.standard_normal((nits - 1, P, W)), rs.rand(nits - 1, W)))
+    else:
+        kw.update(rng="numpy", numpy_seeds=np.arange(W) + 11, prior_draws=2)
+    eng = m.engine()
+    seq = _np(eng.mh_run(theta, y0, **kw))
+    assert eng.last_mh_depth() == 0
+    spec = _np(eng.mh_run(theta, y0, speculate=depth, **kw))
+    d = eng.last_mh_depth()
+    assert d == depth if depth != "auto" else d >= 8
+    _equal(spec, seq)
+    acc = seq["final"][3]
+    assert (acc > 0).any() and (acc < nits - 1).any()  # both branches of the tree were taken
+
+
+def test_rk4_speculative_state0_parameter_vs_c_restatement():
+    """one_i with a 'V0' initial-condition parameter (the linked state follows the
+    accepted parameter), replay draws: speculative rounds vs the C restatement of the
+    sequential chain (rtol 1e-11: ocml vs libm log/exp) and bitwise vs speculate=0."""
+    m, P, theta, y0 = _inputs("one_i", 67, extra={"V0": 10981000.0})
+    nits = 25
+    rs = np.random.RandomState(2)
+    dz = 0.05 * rs.standard_normal((nits - 1, P, 67))
+    u = rs.rand(nits - 1, 67)
+    init_param = [-1, -1, 4]
+    walk = np.ones(P, np.uint8)
+    kw = dict(nits=nits, burnin=10, walk_mask=walk, init_param=init_param, rng="replay", replay=(dz, u))
+    eng = m.engine()
+    spec = _np(eng.mh_run(theta, y0, speculate=4, **kw))
+    _equal(spec, _np(eng.mh_run(theta, y0, **kw)))
+    ref = rk_ref.mh_run(m.fit_problem(), theta, y0, nits, 10, walk, init_param=init_param, rng="replay",
+                        replay=(dz, u))
+    np.testing.assert_allclose(spec["samples"], ref["samples"], rtol=1e-11)
+    np.testing.assert_allclose(spec["y0"], ref["y0"], rtol=1e-11)
+    np.testing.assert_array_equal(spec["y0"][2], spec["theta"][4])
+
+
+@pytest.mark.parametrize("method", ["dopri5", "auto"])
+def test_dopri5_speculative_chains_take_the_sequential_decisions(method):
+    """DOPRI5 / auto: the same accept/reject decisions as speculate=0 (so the parameters,
+    iterations and acceptance ratios are bitwise equal) and chi / R² / AIC within rtol 1e-7
+    (the proposals share waves with other proposals: another step-size sequence, each
+    within the 1.49e-8 tolerance)."""
+    m, P, theta, y0 = _inputs("two_i", 24, method)
+    walk = np.ones(P, np.uint8)
+    kw = dict(nits=40, burnin=15, walk_mask=walk, rng="philox", seed=21)
+    eng = m.engine()
+    seq = _np(eng.mh_run(theta, y0, **kw))
+    spec = _np(eng.mh_run(theta, y0, speculate="auto", **kw))
+    assert eng.last_mh_depth() >= 8
+    for c in list(range(P)) + [P + 3, P + 4]:  # parameters, iteration, acceptance ratio
+        assert np.array_equal(spec["samples"][:, c], seq["samples"][:, c]), c
+    np.testing.assert_allclose(spec["samples"][:, P:P + 3], seq["samples"][:, P:P + 3], rtol=1e-7)
+    assert np.array_equal(spec["theta"], seq["theta"])
+    np.testing.assert_allclose(spec["final"], seq["final"], rtol=1e-7)
+    assert np.array_equal(spec["status"], seq["status"])
+
+
+def test_speculative_resume_equals_one_run():
+    """A speculative run stopped at iteration 12 and resumed gives the uninterrupted run
+    (rounds restart at the resume point; draws are indexed by iteration)."""
+    m, P, theta, y0 = _inputs("two_i", 9)
+    walk = np.ones(P, np.uint8)
+    kw = dict(walk_mask=walk, rng="philox", seed=8, speculate=3)
+    eng = m.engine()
+    full = _np(eng.mh_run(theta, y0, nits=30, burnin=5, **kw))
+    part = eng.mh_run(theta, y0, nits=12, burnin=5, **kw)
+    rest = _np(eng.mh_run(None, None, nits=30, burnin=5, resume=part, **kw))
+    np.testing.assert_array_equal(np.concatenate([part["samples"].cpu().numpy(), rest["samples"]]), full["samples"])
+    for k in ("theta", "y0", "final", "status"):
+        np.testing.assert_array_equal(rest[k], full[k])
+
+
+def test_speculation_depth_rule_and_edges():
+    """The library's depth: (2^d - 1)·W lanes within about one wave per SIMD, none when the
+    chains fill the device; all-static chains and burn-in past the end behave as
+    speculate=0."""
+    m, P, theta, y0 = _inputs("two_i", 4096)
+    eng = m.engine()
+    walk = np.ones(P, np.uint8)
+    eng.mh_run(theta, y0, nits=3, burnin=0, walk_mask=walk, speculate="auto")
+    assert 2 <= eng.last_mh_depth() <= 5
+    big = np.repeat(theta[:, :1], 131072, axis=1)
+    eng.mh_run(big, np.repeat(y0[:, :1], 131072, axis=1), nits=2, burnin=0, walk_mask=walk, speculate="auto")
+    assert eng.last_mh_depth() == 0
+    th, yy = theta[:, :6], y0[:, :6]
+    for walk_mask, burnin in ((np.zeros(P, np.uint8), 2), (walk, 40)):
+        kw = dict(nits=9, burnin=burnin, walk_mask=walk_mask, rng="philox", seed=1)
+        _equal(_np(eng.mh_run(th, yy, speculate=3, **kw)), _np(eng.mh_run(th, yy, **kw)))
