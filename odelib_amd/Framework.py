@@ -507,14 +507,16 @@ class ModelFramework:
 
     def MCMC(self, chain_inits=1, iterations_per_chain=1000, cpu_cores=1, static_parameters=list(),
              print_report=True, fitsurvey_samples=1000, sd_fitdistance=3.0, rng='replay', seed=0,
-             print_iterations=True):
+             print_iterations=True, speculate="auto"):
         """Markov chain Monte Carlo over all chains at once (Framework.py:946-1061).
 
         Each chain is one walker of a single batched ``oe_mh_run``; chain i keeps the
         reference's seed i (Framework.py:1015/1020).  ``cpu_cores`` only shapes the fit
         survey's row order, as the reference's workers would.  ``print_iterations``
         (new): the reference's chains print ``it exp(-chi)`` on every iteration
-        (Samplers.py:123), chain after chain; pass False for large ensembles."""
+        (Samplers.py:123), chain after chain; pass False for large ensembles.
+        ``speculate`` (new): speculative MH rounds while the chains leave the device idle
+        (``Samplers.batched_metropolis_hastings``); 0 = one iteration per step."""
         if isinstance(chain_inits, pd.DataFrame):
             chain_inits = [row.to_dict() for _, row in chain_inits[self.get_pnames()].iterrows()]
         if isinstance(chain_inits, int):
@@ -527,7 +529,7 @@ class ModelFramework:
         posterior = Samplers.batched_metropolis_hastings(
             chains, nits=iterations_per_chain, burnin=int(iterations_per_chain / 2),
             static_parameters=static_parameters, rng=rng, seed=seed, engine=self.engine(),
-            iteration_log=print_iterations)
+            iteration_log=print_iterations, speculate=speculate)
         print('not working')
         if print_report:
             self._print_fit_report(posterior)

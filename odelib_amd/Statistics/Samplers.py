@@ -105,7 +105,7 @@ def _print_iterations(a_priori, chi_rows):
 
 def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameters=(), rng="replay", seed=0,
                                 engine=None, walker_offset=0, return_device=False, iteration_log=False,
-                                print_prior=False):
+                                print_prior=False, speculate="auto"):
     """Run ``len(chains)`` Metropolis–Hastings chains as walkers of one device launch.
 
     chains : ModelFramework copies (one per chain, each with its own initial θ,
@@ -114,7 +114,11 @@ def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameter
              then keeps every iteration's row on the device and drops the burn-in rows
              on the host: same chains, the kernel's arithmetic does not depend on burnin).
     print_prior : print the reference's ``a priori error`` line and header first
-             (MetropolisHastings with print_progress, Samplers.py:101-103)."""
+             (MetropolisHastings with print_progress, Samplers.py:101-103).
+    speculate : speculative MH rounds (``Engine.mh_run``): "auto" lets the library run
+             several iterations per launch while the chains leave the device mostly idle
+             (a few to a few thousand chains) — the same chains, the same decisions; 0
+             runs one iteration per step."""
     m0 = chains[0]
     pnames = m0.get_pnames()
     snames = list(m0._snames)
@@ -142,7 +146,7 @@ def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameter
             rng = "replay"
             replay = legacy_replay_streams(seeds, nits, pnames, walking, dists, oldvals=theta.T.tolist())
     kw = dict(walk_mask=walk, init_param=init_param, rng=rng, seed=seed, replay=replay, walker_offset=walker_offset,
-              numpy_seeds=numpy_seeds, prior_draws=prior_draws)
+              numpy_seeds=numpy_seeds, prior_draws=prior_draws, speculate=speculate)
     logging = (iteration_log or print_prior) and not return_device
     a_priori = None
     if logging:  # the a-priori state's chi: the kernel's own first integration (nits = 1)

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--chains", nargs="+", type=int, default=[32, 1024, 8192])
     ap.add_argument("--iterations", type=int, default=1000)
     ap.add_argument("--method", default=None, help="engine method (default: the drop-in default, 'auto')")
+    ap.add_argument("--speculate", nargs="+", default=["auto"], help="MCMC speculate values to time (auto, 0, d)")
     args = ap.parse_args()
     import pandas as pd
     import scipy.stats
@@ -79,15 +80,17 @@ def main():
     m.MCMC(chain_inits=2, iterations_per_chain=10, print_report=False, fitsurvey_samples=200, sd_fitdistance=6.0,
            print_iterations=False)
     torch.cuda.synchronize()
-    for n in args.chains:
+    for n, spec in ((n, s) for n in args.chains for s in args.speculate):
+        spec = spec if spec == "auto" else int(spec)
         split.clear()
         t0 = time.perf_counter()
         post = m.MCMC(chain_inits=n, iterations_per_chain=args.iterations, cpu_cores=8, print_report=False,
-                      fitsurvey_samples=10000, sd_fitdistance=6.0, print_iterations=False)
+                      fitsurvey_samples=10000, sd_fitdistance=6.0, print_iterations=False, speculate=spec)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         med = {p: float(rawstats(post[p])[0]) for p in priors}
-        print(json.dumps({"chains": n, "iterations_per_chain": args.iterations, "wall_s": round(wall, 3),
+        print(json.dumps({"chains": n, "speculate": spec, "depth": eng.last_mh_depth(),
+                          "iterations_per_chain": args.iterations, "wall_s": round(wall, 3),
                           "posterior_rows": int(len(post)), "chains_in_posterior": int(post["chain#"].nunique()),
                           "acceptance_ratio_mean": float(post.groupby("chain#")["acceptance_ratio"].last().mean()),
                           "method": m.method, "split": {k: round(v, 3) for k, v in split.items()},
