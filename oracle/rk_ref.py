@@ -163,3 +163,101 @@ def philox4x32_10(ctr, key):
     out = np.empty(4, np.uint32)
     lib().ref_philox4x32_10(_p(c), _p(k), _p(out))
     return out
+
+
+def philox_draws(seed, gid, it, P, step_sd):
+    """(step_sd·z [P], u) of walker ``gid`` at iteration ``it`` (the MH kernel's Philox draws)."""
+    z = np.empty(P + 1)
+    u = np.empty(1)
+    lib().ref_philox_draws(int(seed) & 0xFFFFFFFFFFFFFFFF, int(gid), int(it), int(P), _p(z), _p(u))
+    return step_sd * z[:P], float(u[0])
+
+
+def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3, rng="philox", seed=0,
+                replay=None, step_sd=0.05, walker_offset=0, chunk=25):
+    """The speculative MH rounds of oe_mh_run (oe_mh_args.speculate = depth; ode_kernels.cuh
+    k_mh_tree / capi.hip k_mh_resolve) restated on top of this restatement's batched
+    integrate: per round of d iterations the (2^d - 1)·W proposals (node-major lanes, node n
+    at depth floor(log2(n+1)), path bits n + 1 - 2^depth) are integrated in ONE call —
+    the same lockstep grouping as the device lanes — then each chain walks its tree with
+    the accept test exp(log(exp(chi - chin))) > u (Samplers.py:124-153).  Rounds restart at
+    the device's chunk boundaries (chunk rounded down to a multiple of d).  Proposals use
+    numpy's exp/log (the device: ocml), hence rtol-level, not bitwise, agreement."""
+    pr = Problem(fp)
+    S, P = pr.S, pr.P
+    theta = np.array(theta, dtype=np.float64, copy=True)
+    y0 = np.array(y0, dtype=np.float64, copy=True)
+    W = theta.shape[1]
+    walk = np.asarray(walk_mask, bool)
+    ip = np.full(S, -1) if init_param is None else np.asarray(init_param)
+    any_walk = walk.any()
+    a0 = integrate(fp, y0, theta, trajectory=False, split=1)
+    chi = a0["chi"].copy()
+    rsq = 1.0 - a0["ssres"] / pr.sstot
+    aic = -2.0 * (-chi) + 2.0 * pr.pnum
+    nacc = np.zeros(W)
+    status = a0["status"].copy()
+    dz = np.empty((nits, P, W))
+    uu = np.empty((nits, W))
+    for it in range(1, nits):
+        if rng == "philox":
+            for w in range(W):
+                dz[it, :, w], uu[it, w] = philox_draws(seed, walker_offset + w, it, P, step_sd)
+        else:
+            dz[it], uu[it] = replay[0][it - 1], replay[1][it - 1]
+    kept = max(0, nits - 1 - burnin)
+    samples = np.empty((max(kept, 1), P + 5, W))
+    chunk = max(depth, chunk // depth * depth)
+    for c0 in range(1, nits, chunk):
+        c1 = min(nits, c0 + chunk)
+        r0 = c0
+        while r0 < c1:
+            d = min(depth, c1 - r0)
+            N = (1 << d) - 1
+            tn = np.empty((N, P, W))
+            for n in range(N):
+                j = int(np.floor(np.log2(n + 1)))
+                path = n + 1 - (1 << j)
+                th = theta.copy()
+                for k in range(j):
+                    if (path >> k) & 1:
+                        th[walk] = np.exp(np.log(th[walk]) + dz[r0 + k][walk])
+                t = th.copy()
+                t[walk] = np.exp(np.log(th[walk]) + dz[r0 + j][walk])
+                tn[n] = t
+            ys = np.repeat(y0[None], N, axis=0)
+            if any_walk:
+                for s in range(S):
+                    if ip[s] >= 0:
+                        ys[:, s] = tn[:, ip[s]]
+            res = integrate(fp, np.ascontiguousarray(ys.transpose(1, 0, 2).reshape(S, N * W)),
+                            np.ascontiguousarray(tn.transpose(1, 0, 2).reshape(P, N * W)), trajectory=False, split=1)
+            nchi = res["chi"].reshape(N, W)
+            nss = res["ssres"].reshape(N, W)
+            nst = res["status"].reshape(N, W)
+            for w in range(W):
+                path = 0
+                for j in range(d):
+                    it = r0 + j
+                    n = (1 << j) - 1 + path
+                    with np.errstate(over="ignore", invalid="ignore"):
+                        acc = bool(np.exp(np.log(np.exp(chi[w] - nchi[n, w]))) > uu[it, w])
+                    if acc:
+                        chi[w] = nchi[n, w]
+                        rsq[w] = 1.0 - nss[n, w] / pr.sstot
+                        aic[w] = -2.0 * (-chi[w]) + 2.0 * pr.pnum
+                        nacc[w] += 1.0
+                        theta[:, w] = tn[n, :, w]
+                        status[w] = nst[n, w]
+                    if any_walk:
+                        for s in range(S):
+                            if ip[s] >= 0:
+                                y0[s, w] = theta[ip[s], w]
+                    if it > burnin:
+                        row = samples[it - burnin - 1]
+                        row[:P, w] = theta[:, w]
+                        row[P:, w] = (chi[w], rsq[w], aic[w], it, nacc[w] / it)
+                    path |= int(acc) << j
+            r0 += d
+    final = np.stack([chi, rsq, aic, nacc])
+    return {"samples": samples[:kept], "theta": theta, "y0": y0, "final": final, "status": status}

@@ -140,3 +140,23 @@ def test_speculation_depth_rule_and_edges():
     for walk_mask, burnin in ((np.zeros(P, np.uint8), 2), (walk, 40)):
         kw = dict(nits=9, burnin=burnin, walk_mask=walk_mask, rng="philox", seed=1)
         _equal(_np(eng.mh_run(th, yy, speculate=3, **kw)), _np(eng.mh_run(th, yy, **kw)))
+
+
+@pytest.mark.parametrize("method", ["rk4", "dopri5", "auto"])
+def test_speculative_rounds_vs_c_restatement(method):
+    """Device rounds vs their C restatement (rk_ref.mh_tree_run: the round's proposals
+    integrated by the restatement's batched integrate in the device's node-major lane order,
+    hence the same DOPRI5 lockstep groups): rtol 1e-11 for RK4, 1e-8 for DOPRI5 / auto
+    (ocml vs libm exp/log in the proposals), status bitwise; one static parameter, a chunk
+    of 9 iterations (rounds of 4, 4 and 1 per chunk)."""
+    m, P, theta, y0 = _inputs("two_i", 21, method)
+    walk = np.ones(P, np.uint8)
+    walk[3] = 0
+    dev = _np(m.engine().mh_run(theta, y0, nits=20, burnin=6, walk_mask=walk, rng="philox", seed=13, walker_offset=4,
+                                speculate=4, chunk=9))
+    ref = rk_ref.mh_tree_run(m.fit_problem(), theta, y0, 20, 6, walk, depth=4, rng="philox", seed=13,
+                             walker_offset=4, chunk=9)
+    tol = 1e-11 if method == "rk4" else 1e-8
+    for k in ("samples", "theta", "y0", "final"):
+        np.testing.assert_allclose(dev[k], ref[k], rtol=tol, err_msg=k)
+    assert np.array_equal(dev["status"], ref["status"])

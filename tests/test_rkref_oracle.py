@@ -99,3 +99,37 @@ def test_c_mh_replay_matches_oracle_chain_with_same_integrator():
     s = out["samples"][:, :, 0]
     for j, c in enumerate(pn + ["chi", "rsquared", "aic", "iteration", "acceptance_ratio"]):
         np.testing.assert_allclose(s[:, j], ref[c], rtol=1e-11, err_msg=c)
+
+
+@pytest.mark.parametrize("method", ["rk4", "dopri5"])
+def test_c_speculative_rounds_are_the_sequential_chain(method):
+    """The restatement of the speculative MH rounds (rk_ref.mh_tree_run: all 2^d - 1
+    proposals of a round integrated in one batched call, then each chain's path walked)
+    gives the sequential batched MH chain: RK4 to rtol 1e-11 (numpy vs libm exp/log in the
+    proposals), DOPRI5 with the same decisions — hence the same parameters — and chi /
+    R² / AIC within rtol 1e-7 (other lockstep groups)."""
+    m, fp, _, _ = _inputs("two_i")
+    fp.method = method
+    W, nits, burnin = 5, 14, 4
+    P = len(m.get_pnames())
+    theta = np.array([[float(m.parameters[p].val)] for p in m.get_pnames()]) * np.exp(
+        0.02 * np.random.RandomState(3).standard_normal((P, W)))
+    y0 = np.repeat(np.array([[float(m.istates[s])] for s in m._snames]), W, axis=1)
+    walk = np.ones(P, np.uint8)
+    walk[1] = 0
+    seq = rk_ref.mh_run(fp, theta, y0, nits, burnin, walk, rng="philox", seed=6, walker_offset=2)
+    tree = rk_ref.mh_tree_run(fp, theta, y0, nits, burnin, walk, depth=3, rng="philox", seed=6, walker_offset=2,
+                              chunk=7)
+    P5 = P + 5
+    if method == "rk4":
+        for k in ("samples", "theta", "final"):
+            np.testing.assert_allclose(tree[k], seq[k], rtol=1e-11, err_msg=k)
+    else:
+        cols = list(range(P)) + [P + 3, P + 4]
+        np.testing.assert_allclose(tree["samples"][:, cols], seq["samples"][:, cols], rtol=1e-12)
+        np.testing.assert_allclose(tree["samples"][:, P:P + 3], seq["samples"][:, P:P + 3], rtol=1e-7)
+        np.testing.assert_allclose(tree["final"], seq["final"], rtol=1e-7)
+    assert tree["samples"].shape == (nits - 1 - burnin, P5, W)
+    assert np.array_equal(tree["status"], seq["status"])
+    acc = seq["final"][3]
+    assert (acc > 0).any() and (acc < nits - 1).any()
