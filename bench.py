@@ -596,7 +596,39 @@ def extra_configs(args, R, T, P):
             extra[name]["walkers_maxstep"] = int(((stx & 4) != 0).sum())
         del trx, thx, y0t, ex
         torch.cuda.empty_cache()
+    extra.update(small_mcmc(R, T, P))
     return extra
+
+
+def small_mcmc(R, T, P, nits=1001):
+    """The reference's own MCMC shape — few chains, 1000 iterations (the notebook: 32
+    chains) — with one iteration per step and with speculative rounds:
+    wall time of one mh_run each, Philox draws, same chains (parameters compared)."""
+    import numpy as np
+    import torch
+    out = {}
+    for method in ("rk4", "auto"):
+        for W in (32, 1024):
+            ex, y0x = R.engine("two_i", method, T)
+            th = torch.as_tensor(synthetic_walkers(W, P), device=R.dev).contiguous()
+            yy = torch.as_tensor(np.repeat(y0x[:, None], W, axis=1), device=R.dev).contiguous()
+            walk = np.ones(P, np.uint8)
+            row, runs = {}, {}
+            for spec in (0, "auto"):
+                ex.mh_run(th, yy, nits=3, burnin=0, walk_mask=walk, rng="philox", seed=1, speculate=spec)
+                torch.cuda.synchronize(R.dev)
+                t0 = time.perf_counter()
+                runs[spec] = ex.mh_run(th, yy, nits=nits, burnin=nits // 2, walk_mask=walk, rng="philox", seed=5,
+                                       speculate=spec)
+                row[f"wall_s_speculate_{spec}"] = time.perf_counter() - t0
+                row[f"depth_{spec}"] = ex.last_mh_depth()
+            row["speedup"] = row["wall_s_speculate_0"] / row["wall_s_speculate_auto"]
+            row["same_parameters"] = bool(torch.equal(runs[0]["samples"][:, :P], runs["auto"]["samples"][:, :P]))
+            row["workload"] = f"two_i {method} MH, {W} chains x {nits - 1} iterations, Philox, chi only"
+            out[f"MCMC-{W}chains-{method}"] = row
+            del runs, th, yy, ex
+            torch.cuda.empty_cache()
+    return out
 
 
 # ------------------------------------------------------------------ main

@@ -148,7 +148,7 @@ def test_speculative_rounds_vs_c_restatement(method):
     integrated by the restatement's batched integrate in the device's node-major lane order,
     hence the same DOPRI5 lockstep groups): rtol 1e-11 for RK4, 1e-8 for DOPRI5 / auto
     (ocml vs libm exp/log in the proposals), status bitwise; one static parameter, a chunk
-    of 9 iterations (rounds of 4, 4 and 1 per chunk)."""
+    of 9 iterations (rounded down to 8 = two rounds of 4, then a last round of 3)."""
     m, P, theta, y0 = _inputs("two_i", 21, method)
     walk = np.ones(P, np.uint8)
     walk[3] = 0
