@@ -868,7 +868,8 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   // (2^d - 1)·W lanes at most about one wave per SIMD, so a round costs about what one
   // iteration of the few chains costs alone
   int depth = 0;
-  if (a->speculate != 0 && !split && !e->rtc && e->mh_tree[c->method] && a->nits > 1) {
+  const bool has_tree = e->rtc ? e->rtc->mh_tree[c->method] != nullptr : e->mh_tree[c->method] != nullptr;
+  if (a->speculate != 0 && !split && has_tree && a->nits > 1) {
     const int64_t target = (int64_t)64 * 4 * c->n_cu;
     if (a->speculate < 0) {
       depth = 1;
@@ -983,8 +984,7 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       ta.depth = std::min(depth, m.it1 - r0);
       ta.n_lanes = ((int64_t(1) << ta.depth) - 1) * W;
       const dim3 tgrid((unsigned)((ta.n_lanes + kBlock - 1) / kBlock));
-      e->mh_tree[c->method](c->dp, ta, tgrid, block, c->stream);
-      OE_HIP(c, hipGetLastError());
+      OE_HIP(c, launch_mh_tree_entry(e, c->method, c->dp, ta, tgrid, block, c->stream));
       hipLaunchKernelGGL(k_mh_resolve, grid, block, 0, c->stream, c->dp, ta, (int32_t)S);
       OE_HIP(c, hipGetLastError());
     }

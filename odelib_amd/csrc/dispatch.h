@@ -71,6 +71,17 @@ template <class M, int METHOD>
 void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_mh<M, METHOD>), g, b, 0, s, pb, ma);
 }
+inline hipError_t launch_mh_tree_entry(const Entry* e, int method, const DevProblem& dp, const MHTreeArgs& ta,
+                                       dim3 g, dim3 b, hipStream_t s) {
+  if (e->rtc) {
+    DevProblem a0 = dp;
+    MHTreeArgs a1 = ta;
+    void* args[] = {(void*)&a0, (void*)&a1};
+    return hipModuleLaunchKernel(e->rtc->mh_tree[method], g.x, g.y, g.z, b.x, b.y, b.z, 0, s, args, nullptr);
+  }
+  e->mh_tree[method](dp, ta, g, b, s);
+  return hipGetLastError();
+}
 template <class M, int METHOD>
 void launch_mh_tree(const DevProblem& pb, const MHTreeArgs& ta, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_mh_tree<M, METHOD>), g, b, 0, s, pb, ta);

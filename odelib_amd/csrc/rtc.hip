@@ -29,6 +29,9 @@ std::string rtc_integrate_name(int method, int traj, int nt) {
   return std::string("oe::k_integrate<UserModel, ") + kMethodName[method] + ", " + kBool[traj] + ", " + kBool[nt] + ">";
 }
 std::string rtc_mh_name(int method) { return std::string("oe::k_mh<UserModel, ") + kMethodName[method] + ">"; }
+std::string rtc_mh_tree_name(int method) {
+  return std::string("oe::k_mh_tree<UserModel, ") + kMethodName[method] + ">";
+}
 std::string rtc_stiff_wave_name(int traj, int nt) {
   return std::string("oe::k_stiff_wave<UserModel, ") + kBool[traj] + ", " + kBool[nt] + ">";
 }
@@ -52,6 +55,7 @@ std::string rtc_source(const std::string& body, int S, int P, RtcPart part) {
       for (int nt = 0; nt < 2; ++nt)
         src += "template __global__ void " + rtc_integrate_name(m, tr, nt) + "(const oe::DevProblem, const oe::IntegrateArgs);\n";
     src += "template __global__ void " + rtc_mh_name(m) + "(const oe::DevProblem, const oe::MHArgs);\n";
+    src += "template __global__ void " + rtc_mh_tree_name(m) + "(const oe::DevProblem, const oe::MHTreeArgs);\n";
   }
   if (has_stiff_wave(S, part))
     for (int tr = 0; tr < 2; ++tr)
@@ -105,6 +109,7 @@ static std::vector<std::string> all_names(int S, RtcPart part) {
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_integrate_name(m, tr, nt));
   for (int m = m0; m < m0 + 2; ++m) names.push_back(rtc_mh_name(m));
+  for (int m = m0; m < m0 + 2; ++m) names.push_back(rtc_mh_tree_name(m));
   if (has_stiff_wave(S, part))
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_stiff_wave_name(tr, nt));
@@ -149,6 +154,8 @@ int rtc_build(const std::string& body, int S, int P, const char* arch, RtcPart p
         if (!get(&out->integrate[m][tr][nt])) return -1;
   for (int m = m0; m < m0 + 2; ++m)
     if (!get(&out->mh[m])) return -1;
+  for (int m = m0; m < m0 + 2; ++m)
+    if (!get(&out->mh_tree[m])) return -1;
   if (has_stiff_wave(S, part))
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)

@@ -114,3 +114,32 @@ def test_loop_written_chain_model_via_rtc(method, ode):
     for w in (0, 50, 95):
         tight = cpu_ref.odeint_traj(ode, y0[:, w], a.times, theta[:, w], rtol=1e-13, atol=1e-13)
         np.testing.assert_allclose(rb["traj"][:, :, w], tight, rtol=1e-6, atol=1e-4)
+
+
+@pytest.mark.parametrize("method", ["rk4", "auto"])
+def test_rtc_model_speculative_mh(method):
+    """A hipRTC user model (one_i transpiled from the Python callable, forced onto the
+    run-time path) runs the speculative MH rounds too (k_mh_tree from the module,
+    k_mh_resolve from the library): RK4 bitwise its sequential chain, 'auto' (the module's
+    stiff part: the body instantiated with dual numbers) the same decisions; both within
+    the transpiled operand order's rounding of the ahead-of-time model's chains."""
+    a = product_model("one_i", method=method)
+    b = product_model("one_i", method=method, device_model="rtc")
+    W = 12
+    theta = walker_thetas("one_i", W).T.copy()
+    y0 = np.repeat(np.asarray(a.get_inits(), float)[:, None], W, axis=1)
+    walk = np.ones(theta.shape[0], np.uint8)
+    kw = dict(nits=30, burnin=10, walk_mask=walk, rng="philox", seed=4)
+    eb = b.engine()
+    seq = eb.mh_run(theta, y0, **kw)
+    spec = eb.mh_run(theta, y0, speculate="auto", **kw)
+    assert eb.last_mh_depth() >= 8
+    aot = a.engine().mh_run(theta, y0, speculate="auto", **kw)
+    P = theta.shape[0]
+    s_seq, s_spec, s_aot = (r["samples"].cpu().numpy() for r in (seq, spec, aot))
+    if method == "rk4":
+        assert np.array_equal(s_spec, s_seq)
+    else:
+        assert np.array_equal(s_spec[:, :P], s_seq[:, :P])
+        np.testing.assert_allclose(s_spec, s_seq, rtol=1e-7)
+    np.testing.assert_allclose(s_spec, s_aot, rtol=1e-7)
