@@ -346,52 +346,85 @@ __global__ void __launch_bounds__(256) k_philox_draws(const oe::DrawArgs d) {
 // bookkeeping, iteration by iteration, in the reference's arithmetic (Samplers.py:124-153)
 __global__ void __launch_bounds__(256) k_mh_resolve(const oe::DevProblem pb, const oe::MHTreeArgs ta, int32_t S) {
   using namespace oe;
+  constexpr int kMaxD = 16;  // oe_mh_run caps the depth
   const MHArgs& ma = ta.m;
   const int64_t W = ma.W;
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= W) return;
   const int P = pb.P;
   const int PS = P + 5;
+  const int D = ta.depth;
   const uint32_t off = (uint32_t)w * 8u;
   double* cur = ma.cur;
   double chi = Row(cur, W).ld(off), rsq = Row(cur + W, W).ld(off), aic = Row(cur + 2 * W, W).ld(off);
   double nacc = Row(cur + 3 * W, W).ld(off);
+  // 1. the decisions.  The only loads on the path's dependency chain are the node chis; the
+  //    next level's two candidates are loaded before each decision, the uniforms up front.
+  //    exp/log inline (the same ocml functions k_mh calls out of line: the same bits).
+  double uj[kMaxD], cj[kMaxD], rj[kMaxD], aj[kMaxD], nj[kMaxD];
+  int32_t keep[kMaxD];  // node holding the chain's parameters after iteration j (-1: the round's start)
+#pragma unroll
+  for (int j = 0; j < kMaxD; ++j)
+    if (j < D) uj[j] = Row(ma.u + (int64_t)(ma.it0 + j - ma.draw_it0) * W, W).ld(off);
   uint32_t path = 0;
-  for (int j = 0; j < ta.depth; ++j) {
-    const int it = ma.it0 + j;
+  int32_t last = -1;
+  double chin = ta.node_chi[w];
+#pragma unroll
+  for (int j = 0; j < kMaxD; ++j) {
+    if (j >= D) continue;  // (continue, not break: the loop must unroll, the arrays stay in registers)
     const int64_t n = (int64_t)(1u << j) - 1 + path;
-    const double chin = ta.node_chi[n * W + w];
-    const double u = Row(ma.u + (int64_t)(it - ma.draw_it0) * W, W).ld(off);
-    const double lr = oe_exp(chi - chin);
-    const double accp = oe_exp(oe_log(lr));
-    const bool acc = accp > u;
-    // the parameters after this iteration: the proposal if accepted, else the chain's
-    // (read from the node, resp. from θ before anything of this iteration is stored)
-    const double* src = acc ? ta.node_th + n * P * W : ma.theta;
+    double c0 = 0.0, c1 = 0.0;
+    if (j + 1 < D) {
+      const int64_t n0 = (int64_t)(2u << j) - 1 + path;
+      c0 = ta.node_chi[n0 * W + w];
+      c1 = ta.node_chi[(n0 + (int64_t)(1u << j)) * W + w];
+    }
+    const double lr = exp(chi - chin);
+    const double accp = exp(log(lr));
+    const bool acc = accp > uj[j];
     if (acc) {
       chi = chin;
       rsq = 1.0 - ta.node_ss[n * W + w] / pb.sstot;
       aic = -2.0 * (-chi) + 2.0 * (double)pb.pnum;
       nacc += 1.0;
-      for (int q = 0; q < P; ++q) Row(ma.theta + (int64_t)q * W, W).st(off, Row(src + (int64_t)q * W, W).ld(off));
-      if (ma.status) ma.status[w] = ta.node_st[n * W + w];
+      last = (int32_t)n;
     }
-    if (ma.any_walk) {
-      for (int s = 0; s < S; ++s) {
-        const int pi = ma.init_param[s];
-        if (pi >= 0) Row(ma.y0 + (int64_t)s * W, W).st(off, Row(src + (int64_t)pi * W, W).ld(off));
-      }
-    }
-    if (it > ma.burnin) {
-      double* row = ma.samples + (int64_t)(it - ma.row0) * PS * W;
-      for (int q = 0; q < P; ++q) Row(row + (int64_t)q * W, W).st(off, Row(src + (int64_t)q * W, W).ld(off));
-      Row(row + (int64_t)P * W, W).st(off, chi);
-      Row(row + (int64_t)(P + 1) * W, W).st(off, rsq);
-      Row(row + (int64_t)(P + 2) * W, W).st(off, aic);
-      Row(row + (int64_t)(P + 3) * W, W).st(off, (double)it);
-      Row(row + (int64_t)(P + 4) * W, W).st(off, nacc / (double)it);
-    }
+    cj[j] = chi;
+    rj[j] = rsq;
+    aj[j] = aic;
+    nj[j] = nacc;
+    keep[j] = last;
     path |= (acc ? 1u : 0u) << j;
+    chin = acc ? c1 : c0;
+  }
+  // 2. the sample rows (parameters from the node the chain holds, or from θ, which is
+  //    rewritten only after them), then the chain state
+#pragma unroll
+  for (int j = 0; j < kMaxD; ++j) {
+    const int it = ma.it0 + j;
+    if (j >= D || it <= ma.burnin) continue;
+    const double* src = keep[j] >= 0 ? ta.node_th + (int64_t)keep[j] * P * W : ma.theta;
+    double* row = ma.samples + (int64_t)(it - ma.row0) * PS * W;
+    for (int q = 0; q < P; ++q) Row(row + (int64_t)q * W, W).st(off, Row(src + (int64_t)q * W, W).ld(off));
+    Row(row + (int64_t)P * W, W).st(off, cj[j]);
+    Row(row + (int64_t)(P + 1) * W, W).st(off, rj[j]);
+    Row(row + (int64_t)(P + 2) * W, W).st(off, aj[j]);
+    Row(row + (int64_t)(P + 3) * W, W).st(off, (double)it);
+    Row(row + (int64_t)(P + 4) * W, W).st(off, nj[j] / (double)it);
+  }
+  if (last >= 0) {
+    const double* src = ta.node_th + (int64_t)last * P * W;
+    for (int q = 0; q < P; ++q) Row(ma.theta + (int64_t)q * W, W).st(off, Row(src + (int64_t)q * W, W).ld(off));
+    if (ma.status) ma.status[w] = ta.node_st[(int64_t)last * W + w];
+  }
+  // linked initial states follow the current parameters (k_mh stores them every iteration:
+  // the same final values)
+  if (ma.any_walk) {
+    const double* src = last >= 0 ? ta.node_th + (int64_t)last * P * W : ma.theta;
+    for (int s = 0; s < S; ++s) {
+      const int pi = ma.init_param[s];
+      if (pi >= 0) Row(ma.y0 + (int64_t)s * W, W).st(off, Row(src + (int64_t)pi * W, W).ld(off));
+    }
   }
   Row(cur, W).st(off, chi);
   Row(cur + W, W).st(off, rsq);
