@@ -220,8 +220,9 @@ typedef struct {
                                  in the same order.  RK4: bitwise the chains of speculate = 0;
                                  DOPRI5 / auto: within the integration tolerance (a wave's 64
                                  lanes share one step size, and they are other proposals here).
-                                 One-lane MH kernels, built-in and hipRTC models (ignored for the
-                                 split DOPRI5 kernels of the wide built-in chains). */
+                                 Every MH kernel: built-in and hipRTC models, one lane or split
+                                 over K lanes per chain (the depth then counts K lanes per
+                                 proposal). */
 } oe_mh_args;
 
 int oe_abi_version(void);

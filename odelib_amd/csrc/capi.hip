@@ -901,9 +901,11 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   // (2^d - 1)·W lanes at most about one wave per SIMD, so a round costs about what one
   // iteration of the few chains costs alone
   int depth = 0;
-  const bool has_tree = e->rtc ? e->rtc->mh_tree[c->method] != nullptr : e->mh_tree[c->method] != nullptr;
-  if (a->speculate != 0 && !split && has_tree && a->nits > 1) {
-    const int64_t target = (int64_t)64 * 4 * c->n_cu;
+  const bool has_tree = split ? e->mh_split_tree != nullptr
+                       : e->rtc ? e->rtc->mh_tree[c->method] != nullptr : e->mh_tree[c->method] != nullptr;
+  const int lanes_per_walker = split ? e->split_lanes : 1;
+  if (a->speculate != 0 && has_tree && a->nits > 1) {
+    const int64_t target = (int64_t)64 * 4 * c->n_cu / lanes_per_walker;
     if (a->speculate < 0) {
       depth = 1;
       while (depth < 16 && ((int64_t(1) << (depth + 1)) - 1) * W <= target) ++depth;
@@ -1016,8 +1018,13 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       ta.m.it0 = r0;
       ta.depth = std::min(depth, m.it1 - r0);
       ta.n_lanes = ((int64_t(1) << ta.depth) - 1) * W;
-      const dim3 tgrid((unsigned)((ta.n_lanes + kBlock - 1) / kBlock));
-      OE_HIP(c, launch_mh_tree_entry(e, c->method, c->dp, ta, tgrid, block, c->stream));
+      const dim3 tgrid((unsigned)((ta.n_lanes * lanes_per_walker + kBlock - 1) / kBlock));
+      if (split) {
+        e->mh_split_tree(c->dp, ta, tgrid, block, c->stream);
+        OE_HIP(c, hipGetLastError());
+      } else {
+        OE_HIP(c, launch_mh_tree_entry(e, c->method, c->dp, ta, tgrid, block, c->stream));
+      }
       hipLaunchKernelGGL(k_mh_resolve, grid, block, 0, c->stream, c->dp, ta, (int32_t)S);
       OE_HIP(c, hipGetLastError());
     }

@@ -31,6 +31,7 @@ struct Entry {
   StiffWaveLaunch stiff_wave[2][2];  // [traj][nt]: S > kStiffRegS stiff redo, one wave per walker
   IntegrateLaunch dopri5_split[2][2];  // [traj][nt]: DOPRI5 with split_lanes lanes per walker (split.cuh)
   MHLaunch mh_split = nullptr;         // DOPRI5 Metropolis–Hastings, split_lanes lanes per walker
+  MHTreeLaunch mh_split_tree = nullptr;  // its speculative rounds (k_mh_split_tree)
   int32_t split_lanes = 0;             // 0: the model has no split kernel
   const RtcModule* rtc = nullptr;  // user RHS compiled at run time (launchers above unused)
 };
@@ -110,6 +111,10 @@ template <int N, int K>
 void launch_mh_split(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_mh_split<N, K>), g, b, 0, s, pb, ma);
 }
+template <int N, int K>
+void launch_mh_split_tree(const DevProblem& pb, const MHTreeArgs& ta, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_mh_split_tree<N, K>), g, b, 0, s, pb, ta);
+}
 // lanes per walker of a model's split DOPRI5 kernel (split.cuh): the built-in chain only
 template <class M>
 struct SplitOf { static constexpr int K = 0; };
@@ -156,6 +161,7 @@ Entry make_entry(int32_t model_id) {
     e.dopri5_split[1][0] = launch_split<M::S, K, true, false>;
     e.dopri5_split[1][1] = launch_split<M::S, K, true, true>;
     e.mh_split = launch_mh_split<M::S, K>;
+    e.mh_split_tree = launch_mh_split_tree<M::S, K>;
   }
   if constexpr (M::S <= OE_PIPE_MAX_S) {
     e.rk4_piped[0][0] = launch_rk4_piped<M, false, 2>;

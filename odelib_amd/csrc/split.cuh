@@ -555,3 +555,73 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 }
 
 }  // namespace oe
+
+namespace oe {
+
+// Speculative MH rounds (k_mh_tree, ode_kernels.cuh) for the split DOPRI5 models: a
+// (node, chain) pair on K adjacent lanes, node-major, every lane forming the node's
+// proposal from the chain's θ (the same values on every lane) and integrating its m
+// states; lane 0 stores the node's result.  k_mh_resolve is shared.
+template <int N, int K>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+    k_mh_split_tree(const DevProblem pb, const MHTreeArgs ta) {
+  constexpr int m = N / K;
+  constexpr int PMAX = 5 + 4;
+  const MHArgs& ma = ta.m;
+  const int64_t W = ma.W;
+  const int P = pb.P;
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = (int)(threadIdx.x & (K - 1));
+  const int64_t gl = gt / K;
+  const bool active = gl < ta.n_lanes;
+  const int64_t g = active ? gl : ta.n_lanes - 1;
+  const int64_t n = g / W;
+  const int64_t c = g - n * W;
+  const int j = 31 - __builtin_clz((uint32_t)(n + 1));
+  const uint32_t path = (uint32_t)(n + 1) - (1u << j);
+  const uint32_t off = (uint32_t)c * 8u;
+  const uint32_t off_s = (uint32_t)(c * 8 + (int64_t)r * m * W * 8);  // this lane's first state in [N][W]
+  const Row ys(ma.y0, (int64_t)N * W);
+  double th[PMAX];
+#pragma unroll
+  for (int q = 0; q < PMAX; ++q) th[q] = (q < P) ? Row(ma.theta + (int64_t)q * W, W).ld(off) : 0.0;
+  for (int k = 0; k < j; ++k) {
+    if (!((path >> k) & 1u)) continue;
+    const double* dz = ma.dz + (int64_t)(ma.it0 + k - ma.draw_it0) * P * W;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q)
+      if (q < P && ((ma.walk_mask >> q) & 1ull)) th[q] = oe_exp(oe_log(th[q]) + Row(dz + (int64_t)q * W, W).ld(off));
+  }
+  double tn[PMAX];
+  {
+    const double* dz = ma.dz + (int64_t)(ma.it0 + j - ma.draw_it0) * P * W;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q)
+      tn[q] = (q < P && ((ma.walk_mask >> q) & 1ull)) ? oe_exp(oe_log(th[q]) + Row(dz + (int64_t)q * W, W).ld(off))
+                                                      : th[q];
+  }
+  double y[m], p5[5];
+#pragma unroll
+  for (int jj = 0; jj < m; ++jj) {
+    int pi = ma.init_param[jj];
+#pragma unroll
+    for (int q = 1; q < K; ++q) pi = (r == q) ? ma.init_param[q * m + jj] : pi;
+    y[jj] = (ma.any_walk && pi >= 0) ? pick(tn, pi) : ys.ld(off_s + (uint32_t)(jj * W * 8));
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) p5[q] = tn[q];
+  Acc a = acc_init();
+  integrate_dopri5_split<N, K, false, false>(pb, y, p5, nullptr, ta.n_lanes, 0u, active, r, a);
+  if (active && r == 0) {
+    const int64_t NW = ta.n_lanes;
+    const uint32_t o = (uint32_t)g * 8u;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q)
+      if (q < P) Row(ta.node_th + n * P * W + (int64_t)q * W, W).st(off, tn[q]);
+    Row(ta.node_chi, NW).st(o, a.nvalid ? a.chi : __builtin_nan(""));
+    Row(ta.node_ss, NW).st(o, a.ssres);
+    ta.node_st[g] = finish(a);
+  }
+}
+
+}  // namespace oe

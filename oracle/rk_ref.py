@@ -174,7 +174,7 @@ def philox_draws(seed, gid, it, P, step_sd):
 
 
 def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3, rng="philox", seed=0,
-                replay=None, step_sd=0.05, walker_offset=0, chunk=25):
+                replay=None, step_sd=0.05, walker_offset=0, chunk=25, split=None):
     """The speculative MH rounds of oe_mh_run (oe_mh_args.speculate = depth; ode_kernels.cuh
     k_mh_tree / capi.hip k_mh_resolve) restated on top of this restatement's batched
     integrate: per round of d iterations the (2^d - 1)·W proposals (node-major lanes, node n
@@ -182,8 +182,11 @@ def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3
     the same lockstep grouping as the device lanes — then each chain walks its tree with
     the accept test exp(log(exp(chi - chin))) > u (Samplers.py:124-153).  Rounds restart at
     the device's chunk boundaries (chunk rounded down to a multiple of d).  Proposals use
-    numpy's exp/log (the device: ocml), hence rtol-level, not bitwise, agreement."""
+    numpy's exp/log (the device: ocml), hence rtol-level, not bitwise, agreement.
+    ``split`` as in ``mh_run`` (the split DOPRI5 models' rounds put a proposal on K lanes:
+    64/K proposals per step size)."""
     pr = Problem(fp)
+    split = product_split(fp) if split is None else int(split)
     S, P = pr.S, pr.P
     theta = np.array(theta, dtype=np.float64, copy=True)
     y0 = np.array(y0, dtype=np.float64, copy=True)
@@ -191,7 +194,7 @@ def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3
     walk = np.asarray(walk_mask, bool)
     ip = np.full(S, -1) if init_param is None else np.asarray(init_param)
     any_walk = walk.any()
-    a0 = integrate(fp, y0, theta, trajectory=False, split=1)
+    a0 = integrate(fp, y0, theta, trajectory=False, split=split)
     chi = a0["chi"].copy()
     rsq = 1.0 - a0["ssres"] / pr.sstot
     aic = -2.0 * (-chi) + 2.0 * pr.pnum
@@ -231,7 +234,8 @@ def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3
                     if ip[s] >= 0:
                         ys[:, s] = tn[:, ip[s]]
             res = integrate(fp, np.ascontiguousarray(ys.transpose(1, 0, 2).reshape(S, N * W)),
-                            np.ascontiguousarray(tn.transpose(1, 0, 2).reshape(P, N * W)), trajectory=False, split=1)
+                            np.ascontiguousarray(tn.transpose(1, 0, 2).reshape(P, N * W)), trajectory=False,
+                            split=split)
             nchi = res["chi"].reshape(N, W)
             nss = res["ssres"].reshape(N, W)
             nst = res["status"].reshape(N, W)

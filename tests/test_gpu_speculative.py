@@ -160,3 +160,41 @@ def test_speculative_rounds_vs_c_restatement(method):
     for k in ("samples", "theta", "y0", "final"):
         np.testing.assert_allclose(dev[k], ref[k], rtol=tol, err_msg=k)
     assert np.array_equal(dev["status"], ref["status"])
+
+
+@pytest.mark.parametrize("n,K", [(20, 2), (24, 4)])
+def test_split_dopri5_speculative_rounds(n, K):
+    """The wide chain models' split DOPRI5 MH (a chain on K lanes) in speculative rounds
+    (k_mh_split_tree): the same decisions as the sequential split kernel, chi / R² / AIC
+    within rtol 1e-7, and vs the C restatement of the rounds with the same 64/K grouping
+    at rtol 1e-8; a '<state>0' parameter linking the last state (held by lane K-1)."""
+    from odelib_amd import ModelFramework, parameter
+    from helpers import THETA, chain_rhs, demo_df
+    snames = ["S"] + [f"I{k}" for k in range(1, n - 1)] + ["V"]
+    th = dict(THETA["two_i"], V0=10981000.0)
+    m = ModelFramework(ODE=chain_rhs(n), parameter_names=list(th), state_names=snames,
+                       dataframe=demo_df({"virus": "V", "host": "H"}), state_summations={"H": snames[:-1]},
+                       t_steps=1000, S=5236900, method="dopri5", device_model="chain",
+                       **{p: parameter(init_value=v) for p, v in th.items()})
+    fp = m.fit_problem()
+    assert rk_ref.product_split(fp) == K
+    W, P = 9, len(th)
+    theta = np.array(list(th.values()))[:, None] * np.exp(0.02 * np.random.RandomState(6).standard_normal((P, W)))
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    init_param = np.full(n, -1, np.int32)
+    init_param[n - 1] = 5
+    walk = np.ones(P, np.uint8)
+    kw = dict(nits=18, burnin=5, walk_mask=walk, init_param=init_param, rng="philox", seed=17, chunk=8)
+    eng = m.engine()
+    seq = _np(eng.mh_run(theta, y0, **kw))
+    spec = _np(eng.mh_run(theta, y0, speculate=4, **kw))
+    assert eng.last_mh_depth() == 4
+    for c in list(range(P)) + [P + 3, P + 4]:
+        assert np.array_equal(spec["samples"][:, c], seq["samples"][:, c]), c
+    np.testing.assert_allclose(spec["samples"], seq["samples"], rtol=1e-7)
+    np.testing.assert_array_equal(spec["y0"][n - 1], spec["theta"][5])
+    ref = rk_ref.mh_tree_run(fp, theta, y0, 18, 5, walk, init_param=init_param, depth=4, rng="philox", seed=17,
+                             chunk=8)
+    for k in ("samples", "theta", "y0", "final"):
+        np.testing.assert_allclose(spec[k], ref[k], rtol=1e-8, err_msg=k)
+    assert (seq["final"][3] > 0).any()
