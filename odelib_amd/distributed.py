@@ -82,17 +82,20 @@ def native_allgather_walkers(block, n_total: int, comm):
 
 
 def sharded_mh(engine, theta_all, y0_all, nits: int, burnin: int, walk_mask, init_param=None, seed: int = 0,
-               step_sd: float = 0.05, group=None):
+               step_sd: float = 0.05, group=None, speculate="auto"):
     """Run the global ensemble ``theta_all [P][W_total]`` sharded over the ranks of
     ``group`` (each rank: its shard on its own device via ``engine``), Philox draws, and
-    return the pooled posterior samples [kept][P+5][W_total] (identical on all ranks)."""
+    return the pooled posterior samples [kept][P+5][W_total] (identical on all ranks).
+    ``speculate``: each rank's speculative MH rounds (``Engine.mh_run``; on for shards too
+    small to fill their device) — the draws are keyed by global walker id and iteration, so
+    the chains are those of one sequential launch either way."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     W = int(np.asarray(theta_all).shape[1]) if not hasattr(theta_all, "shape") else int(theta_all.shape[1])
     off, cnt = shard(W, rank, world)
     r = engine.mh_run(theta_all[:, off:off + cnt], y0_all[:, off:off + cnt], nits=nits, burnin=burnin,
                       walk_mask=walk_mask, init_param=init_param, rng="philox", seed=seed, step_sd=step_sd,
-                      walker_offset=off)
+                      walker_offset=off, speculate=speculate)
     return allgather_walkers(r["samples"], W, group=group), r
 
 

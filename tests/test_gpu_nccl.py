@@ -180,8 +180,9 @@ GLOO2_CHILD = textwrap.dedent(r"""
 def test_two_gloo_ranks_device_engine_pool_equals_one_launch():
     """World size 2 with the DEVICE engine (verdict r2: the CPU world-2 test drives the C
     restatement): two ranks on one GPU (gloo; RCCL refuses two ranks per device), each
-    running its shard through oe_mh_run, pooled by the all-gather and the rawstats
-    all-reduces — equal to one 301-walker launch bit for bit."""
+    running its shard through oe_mh_run (in speculative rounds: sharded_mh's default, 151
+    chains leave the device idle), pooled by the all-gather and the rawstats all-reduces —
+    equal to one sequential 301-walker launch bit for bit."""
     port = str(_free_port())
     procs = []
     for r in range(2):
