@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--cases", nargs="+", default=["two_i:65536", "two_i:1048576"])
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--series-ms", type=float, default=40.0, help="length of one timed series")
+    ap.add_argument("--substeps", type=int, default=1, help="rk4_substeps of the problem")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -29,7 +30,7 @@ def main():
     for case in args.cases:
         model, W = case.split(":")
         W = int(W)
-        m, y0h = bench.build_problem(model, "rk4", 1000)
+        m, y0h = bench.build_problem(model, "rk4", 1000, args.substeps)
         theta = torch.as_tensor(bench.synthetic_walkers(W, 5), device=dev).contiguous()
         y0 = torch.as_tensor(np.repeat(y0h[:, None], W, axis=1), device=dev).contiguous()
         eng = m.engine()
@@ -38,7 +39,7 @@ def main():
         t0 = time.perf_counter()
         eng.integrate(y0, theta, traj_out=traj, kernel="auto")
         tune_s = time.perf_counter() - t0
-        row = {"case": case, "auto_choice": eng.last_variant(), "tune_ms": eng.tune_times(),
+        row = {"case": case, "substeps": args.substeps, "auto_choice": eng.last_variant(), "tune_ms": eng.tune_times(),
                "tune_call_s": round(tune_s, 3)}
         avail = [k for k in KERNELS if k in row["tune_ms"]]
 
