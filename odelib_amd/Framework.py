@@ -344,10 +344,13 @@ class ModelFramework:
         return np.ascontiguousarray(np.asarray(rows, dtype=float).reshape(len(rows), len(self._pnames)).T)
 
     # ------------------------------------------------------------------ integration
-    def integrate_batch(self, parameters, inits=None, trajectory=True):
+    def integrate_batch(self, parameters, inits=None, trajectory=True, kernel=None):
         """Batched integrate: ``parameters`` [W][P] (array / DataFrame with pnames
         columns / list of dicts), ``inits`` [W][S] or None (current initial states).
-        Returns the engine dict: traj [T][S][W] (device tensor), chi, ssres, status."""
+        Returns the engine dict: traj [T][S][W] (device tensor), chi, ssres, status.
+        ``kernel="auto"``: for repeated RK4 trajectory batches of one shape, let the
+        library time its trajectory kernels on the first call and keep the fastest
+        (``Engine.integrate``; the first call then takes ~0.2-1 s)."""
         if isinstance(parameters, pd.DataFrame):
             parameters = parameters[self.get_pnames()].to_numpy(dtype=float)
         elif len(parameters) and isinstance(parameters[0], dict):
@@ -358,7 +361,7 @@ class ModelFramework:
             y0 = np.repeat(np.asarray(self.get_inits(), float)[:, None], W, axis=1)
         else:
             y0 = np.ascontiguousarray(np.asarray(inits, float).reshape(W, len(self._snames)).T)
-        return self.engine().integrate(y0, theta, trajectory=trajectory)
+        return self.engine().integrate(y0, theta, trajectory=trajectory, kernel=kernel)
 
     def integrate(self, inits=None, parameters=None, predict_obs=False, as_dataframe=True, sum_subpopulations=True):
         """ModelFramework.integrate (Framework.py:622-683) for one parameter set; the
