@@ -64,6 +64,9 @@ MH_TWO_I_RK4 = ("k_mhINS_4TwoIELi0E",)
 MH_TWO_I_DOPRI5 = ("k_mhINS_4TwoIELi1E",)
 MH_CHAIN20_RK4 = ("k_mhINS_5ChainILi20EEELi0E",)
 MH_CHAIN20_DOPRI5 = ("k_mhINS_5ChainILi20EEELi1E",)
+# speculative MH rounds (k_mh_tree<M, METHOD>): the sequential MH kernel's occupancy
+TREE_TWO_I_RK4 = ("k_mh_treeINS_4TwoIELi0E",)
+TREE_TWO_I_DOPRI5 = ("k_mh_treeINS_4TwoIELi1E",)
 
 
 def test_two_i_kernels_never_spill(resources):
@@ -71,7 +74,8 @@ def test_two_i_kernels_never_spill(resources):
         assert r["scratch"] == 0 and r["vgpr_spill"] == 0, (name, r)
 
 
-@pytest.mark.parametrize("needles,min_occ", [(C1, 4), (C2, 2), (MH_TWO_I_RK4, 4), (MH_TWO_I_DOPRI5, 2)])
+@pytest.mark.parametrize("needles,min_occ", [(C1, 4), (C2, 2), (MH_TWO_I_RK4, 4), (MH_TWO_I_DOPRI5, 2),
+                                             (TREE_TWO_I_RK4, 4), (TREE_TWO_I_DOPRI5, 2)])
 def test_two_i_occupancy(resources, needles, min_occ):
     r = _find(resources["inst_two_i.hip"], *needles)
     assert r["occupancy"] >= min_occ, r
