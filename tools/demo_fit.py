@@ -80,16 +80,27 @@ def main():
     m.MCMC(chain_inits=2, iterations_per_chain=10, print_report=False, fitsurvey_samples=200, sd_fitdistance=6.0,
            print_iterations=False)
     torch.cuda.synchronize()
+    import numpy as np
+    posts = {}
     for n, spec in ((n, s) for n in args.chains for s in args.speculate):
         spec = spec if spec == "auto" else int(spec)
         split.clear()
+        # the chain starts come from the LHS survey and pandas' sample (numpy's global RNG):
+        # seeded alike for every call, so the calls for one chain count run the same chains
+        np.random.seed(20261017 + n)
         t0 = time.perf_counter()
         post = m.MCMC(chain_inits=n, iterations_per_chain=args.iterations, cpu_cores=8, print_report=False,
                       fitsurvey_samples=10000, sd_fitdistance=6.0, print_iterations=False, speculate=spec)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         med = {p: float(rawstats(post[p])[0]) for p in priors}
+        posts[(n, spec)] = post
+        same = None
+        if spec != 0 and (n, 0) in posts:  # the same chains as one iteration per step?
+            ref = posts[(n, 0)]
+            same = bool(np.array_equal(ref[list(priors)].to_numpy(), post[list(priors)].to_numpy()))
         print(json.dumps({"chains": n, "speculate": spec, "depth": eng.last_mh_depth(),
+                          "same_parameters_as_speculate_0": same,
                           "iterations_per_chain": args.iterations, "wall_s": round(wall, 3),
                           "posterior_rows": int(len(post)), "chains_in_posterior": int(post["chain#"].nunique()),
                           "acceptance_ratio_mean": float(post.groupby("chain#")["acceptance_ratio"].last().mean()),
