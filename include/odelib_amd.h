@@ -120,7 +120,8 @@ enum {
                            substeps, store policy, XCD order) runs each candidate back to back
                            after ~60 ms of launches (the clock settles), three interleaved rounds,
                            and keeps the fastest (the default kernel unless another is > 1 %
-                           faster); later calls reuse the choice.  The first call synchronizes
+                           faster); later calls reuse the choice (built-in models: every
+                           context of the process on that device).  The first call synchronizes
                            the stream.  Overrides OE_PIPE*, OE_HALF_WAVES. */
   OE_PIPE_XCD = 16384u  /* with OE_PIPE / OE_PIPE_4 / OE_PIPE_8: the piped kernel's workgroups dealt
                            to the XCDs in runs of 512 walkers (OE_KERNEL_PIPE*X) */

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <memory>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -100,8 +101,10 @@ struct oe_ctx {
   void* tree = nullptr;          // speculative MH rounds: node proposals and results
   size_t tree_bytes = 0;
   int32_t last_mh_depth = 0;     // iterations per round of the last oe_mh_run (0: sequential)
-  // OE_TUNE: the RK4 trajectory kernel chosen per shape, with what was measured
+  // OE_TUNE: the RK4 trajectory kernel chosen per shape, with what was measured (built-in
+  // models: in a process-wide table shared by every context on the device; hipRTC models here)
   struct Tuned {
+    int device;
     const Entry* e;
     int64_t W;
     int32_t T, substeps;
@@ -111,7 +114,8 @@ struct oe_ctx {
   };
   std::vector<Tuned> tuned;
   int32_t last_variant = -1;
-  int32_t last_tuned = -1;  // index into tuned of the last oe_integrate, or -1
+  Tuned last_tune{};          // the choice of the last oe_integrate, if it was tuned
+  bool has_last_tune = false;
 };
 
 namespace {
@@ -262,16 +266,28 @@ hipError_t launch_rk4_traj(oe_ctx* c, const Entry* e, IntegrateArgs ia, int vari
   return launch_integrate_entry(e, OE_METHOD_RK4, 1, nt ? 1 : 0, c->dp, ia, grid, block, c->stream);
 }
 
+// the process-wide OE_TUNE table of the built-in models (their Entry objects are static)
+std::mutex g_tune_mu;
+std::vector<oe_ctx::Tuned> g_tuned;
+
 // OE_TUNE: time every available RK4 trajectory kernel for this shape, back to back, after
-// the clock has settled under load, and remember the fastest.  Returns the cache index.
-int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32_t flags, int dflt, int* idx) {
+// the clock has settled under load, and remember the fastest (per device and shape, for the
+// process: another context on the device reuses the choice).
+int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32_t flags, int dflt,
+             oe_ctx::Tuned* out) {
   const uint32_t mode = (nt ? 1u : 0u) | (flags & (OE_NO_XCD_REMAP | OE_XCD_RANGES));
-  for (size_t i = 0; i < c->tuned.size(); ++i) {
-    const oe_ctx::Tuned& t = c->tuned[i];
-    if (t.e == e && t.W == ia.W && t.T == c->dp.T && t.substeps == c->dp.substeps && t.mode == mode) {
-      *idx = (int)i;
-      return OE_OK;
-    }
+  const bool shared = e->rtc == nullptr;
+  auto match = [&](const oe_ctx::Tuned& t) {
+    return t.device == c->device && t.e == e && t.W == ia.W && t.T == c->dp.T && t.substeps == c->dp.substeps &&
+           t.mode == mode;
+  };
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    for (const oe_ctx::Tuned& t : shared ? g_tuned : c->tuned)
+      if (match(t)) {
+        *out = t;
+        return OE_OK;
+      }
   }
   constexpr int kN = OE_KERNEL_COUNT - 1;
   std::vector<int> cand;
@@ -303,7 +319,7 @@ int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32
     if (rc) return rc;
     settled += ms;
   }
-  oe_ctx::Tuned t{e, ia.W, c->dp.T, c->dp.substeps, mode, dflt, {}};
+  oe_ctx::Tuned t{c->device, e, ia.W, c->dp.T, c->dp.substeps, mode, dflt, {}};
   for (int v = 0; v < kN; ++v) t.ms[v] = HUGE_VAL;
   constexpr int kRounds = 3;
   for (int r = 0; r < kRounds; ++r)
@@ -319,8 +335,11 @@ int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32
   for (int v = 0; v < kN; ++v)
     if (t.ms[v] == HUGE_VAL) t.ms[v] = std::nan("");
   t.variant = best;
-  c->tuned.push_back(t);
-  *idx = (int)c->tuned.size() - 1;
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    (shared ? g_tuned : c->tuned).push_back(t);
+  }
+  *out = t;
   return OE_OK;
 }
 
@@ -731,7 +750,7 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   //   DESIGN.md §6), hence OE_TUNE, which measures them on the device at hand.
   const bool rk4_traj = c->method == OE_METHOD_RK4 && ia.traj;
   int variant = OE_KERNEL_OTHER;
-  c->last_tuned = -1;
+  c->has_last_tune = false;
   if (rk4_traj) {
     const bool auto_half = S >= 5 && W <= (int64_t)64 * 4 * c->n_cu;
     const int dflt = ((flags & OE_HALF_WAVES) || auto_half) ? OE_KERNEL_HALF : OE_KERNEL_DIRECT;
@@ -740,11 +759,10 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
                       : (flags & OE_PIPE) ? OE_KERNEL_PIPE2 + xcd : dflt;
     variant = rk4_variant_ok(e, W, asked, nt, flags) ? asked : dflt;
     if (flags & OE_TUNE) {
-      int idx = -1;
-      rc = tune_rk4(c, e, ia, nt, flags, dflt, &idx);
+      rc = tune_rk4(c, e, ia, nt, flags, dflt, &c->last_tune);
       if (rc) return rc;
-      variant = c->tuned[idx].variant;
-      c->last_tuned = idx;
+      variant = c->last_tune.variant;
+      c->has_last_tune = true;
     }
   }
   c->last_variant = variant;
@@ -1097,8 +1115,8 @@ int oe_last_mh_depth(oe_ctx* c, int32_t* depth) {
 
 int oe_tune_times(oe_ctx* c, double* ms, int32_t n) {
   if (!c || !ms || n < OE_KERNEL_COUNT - 1) return OE_ERR_ARG;
-  if (c->last_tuned < 0) return fail(c, OE_ERR_STATE, "oe_tune_times: the last oe_integrate was not tuned");
-  const oe_ctx::Tuned& t = c->tuned[c->last_tuned];
+  if (!c->has_last_tune) return fail(c, OE_ERR_STATE, "oe_tune_times: the last oe_integrate was not tuned");
+  const oe_ctx::Tuned& t = c->last_tune;
   for (int v = 0; v < OE_KERNEL_COUNT - 1; ++v) ms[v] = t.ms[v];
   return OE_OK;
 }

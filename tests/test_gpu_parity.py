@@ -838,3 +838,23 @@ def test_c_abi_host_pointers_match_device_path(method):
     assert np.array_equal(ssres, dev["ssres"].cpu().numpy())
     assert np.array_equal(st, dev["status"].cpu().numpy())
     assert np.array_equal(chi2, chi, equal_nan=True)
+
+
+def test_tuned_choice_is_shared_by_contexts_on_the_device():
+    """OE_TUNE's table of the built-in models is process-wide: a second engine (its own
+    context) with the same model and shape reuses the first one's measurements instead of
+    tuning again (no ~0.1-0.3 s settle and rounds), and launches the same kernel."""
+    import time
+    theta = _walkers("two_i", 4096)
+    m1, m2 = _model("two_i", "rk4"), _model("two_i", "rk4")
+    y0 = np.repeat(np.asarray(m1.get_inits(), float)[:, None], 4096, axis=1)
+    e1, e2 = m1.engine(), m2.engine()
+    assert e1.ctx is not e2.ctx
+    e1.integrate(y0, theta, kernel="auto")  # tunes (or reuses an earlier test's table entry)
+    t0 = time.perf_counter()
+    r2 = e2.integrate(y0, theta, kernel="auto")
+    dt = time.perf_counter() - t0
+    assert e2.tune_times() == e1.tune_times() and e2.last_variant() == e1.last_variant()
+    assert dt < 0.05, dt  # one launch, no tuning (the settle alone is >= 60 ms of launches)
+    r1 = e1.integrate(y0, theta, kernel="direct")
+    assert np.array_equal(r2["traj"].cpu().numpy(), r1["traj"].cpu().numpy())
