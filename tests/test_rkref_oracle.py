@@ -133,3 +133,23 @@ def test_c_speculative_rounds_are_the_sequential_chain(method):
     assert np.array_equal(tree["status"], seq["status"])
     acc = seq["final"][3]
     assert (acc > 0).any() and (acc < nits - 1).any()
+
+
+def test_c_speculative_rounds_split_grouping():
+    """The restated rounds with the split DOPRI5 grouping (chain16: 2 lanes per chain, 32
+    proposals per step size) take the sequential split chain's decisions: parameters equal,
+    chi / R² / AIC within rtol 1e-7."""
+    m = chain_problem(16, method="dopri5")
+    fp = m.fit_problem()
+    assert rk_ref.product_split(fp) == 2
+    P = len(m.get_pnames())
+    W, nits, burnin = 4, 10, 3
+    theta = np.array([[float(m.parameters[p].val)] for p in m.get_pnames()]) * np.exp(
+        0.02 * np.random.RandomState(5).standard_normal((P, W)))
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    walk = np.ones(P, np.uint8)
+    seq = rk_ref.mh_run(fp, theta, y0, nits, burnin, walk, rng="philox", seed=3)
+    tree = rk_ref.mh_tree_run(fp, theta, y0, nits, burnin, walk, depth=3, rng="philox", seed=3)
+    np.testing.assert_allclose(tree["samples"][:, :P], seq["samples"][:, :P], rtol=1e-12)
+    np.testing.assert_allclose(tree["samples"][:, P:], seq["samples"][:, P:], rtol=1e-7)
+    assert (seq["final"][3] > 0).any()
