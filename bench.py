@@ -297,6 +297,60 @@ def cpu_baseline(model, fp, y0, budget_s, P, procs=None):
                       f"CPU: {_cpu_model()}"}
 
 
+NOTEBOOK_PRIORS = {"mu": {"s": 3, "scale": 1e-8}, "phi": {"s": 3, "scale": 1e-8}, "beta": {"s": 1, "scale": 20},
+                   "lam": {"s": 2, "scale": .1}, "tau": {"s": 2, "scale": 1}}
+
+
+def _oracle_mh_model(m):
+    """oracle.cpu_ref.Model (the reference's MH loop, Samplers.py:53-174) for the product
+    model ``m`` with the notebook's lognorm priors (their pdf/rvs calls are part of the
+    reference's iteration cost)."""
+    import scipy.stats
+    from oracle import cpu_ref
+    from odelib_amd.models import BUILTIN
+    snames = list(m._snames)
+    sidx, out_names, keep, _ = cpu_ref.summation_index(snames, {"H": snames[:-1]})
+    params = {p: cpu_ref.Param(float(v), scipy.stats.lognorm, dict(NOTEBOOK_PRIORS[p]))
+              for p, v in zip(m.get_pnames(), THETA_STAR)}
+    return cpu_ref.Model(BUILTIN["two_i"][3], m.get_pnames(), snames, params, dict(zip(snames, m.get_inits())),
+                         m.times, m._pred_tindex, m._obs_logabundance, m._obs_logsigma, sum_index=sidx,
+                         sumkeep=keep, out_names=out_names)
+
+
+_MH_ORACLE = None
+
+
+def _cpu_mh_worker(args):
+    chains, nits = args
+    from oracle import cpu_ref
+    t0 = time.perf_counter()
+    for c in chains:
+        _MH_ORACLE.random_seed = c
+        cpu_ref.metropolis_hastings(_MH_ORACLE, nits=nits)
+    return len(chains) * (nits - 1), time.perf_counter() - t0
+
+
+def cpu_mcmc_baseline(m, chains=32, nits=101, full_nits=1001):
+    """The reference's MCMC for the small-ensemble entries, on the host cores: the
+    notebook's ``chains`` chains, each the reference's Metropolis-Hastings loop with
+    scipy odeint (oracle/cpu_ref.py), one chain per pool task as Framework.py:779;
+    a bounded sample of ``nits`` iterations per chain, scaled to ``full_nits``."""
+    import multiprocessing as mp
+    global _MH_ORACLE
+    _MH_ORACLE = _oracle_mh_model(m)
+    cores, _ = host_cores()
+    jobs = [([c for c in range(chains) if c % cores == k], nits) for k in range(min(cores, chains))]
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(len(jobs)) as pool:
+        res = pool.map(_cpu_mh_worker, jobs)
+    wall = time.perf_counter() - t0
+    its = sum(r[0] for r in res)
+    return {"wall_s_sample": wall, "chain_iterations_sample": its, "cores": len(jobs),
+            "wall_s_scaled_to_full_run": wall * (full_nits - 1) / (nits - 1),
+            "sample": f"{chains} chains x {nits - 1} iterations of the reference MH loop (scipy odeint, "
+                      f"lognorm priors' pdf/rvs), Pool({len(jobs)}); scaled to {full_nits - 1} iterations"}
+
+
 def cpu_rk4_c(fp, y0, W, cores):
     """The same fixed-step RK4 + fused likelihood in C (oracle/rk_ref.c, OpenMP over
     64-walker groups, interval-major so rows are written as runs of walkers) on the
@@ -655,6 +709,8 @@ def main():
         cpu = cpu_baseline(args.model, fp_host, y0h, args.cpu_seconds, P)
         if args.method == "rk4":
             cpu["rk4_c_openmp"] = cpu_rk4_c(fp_host, y0h, args.walkers, cpu["cores"])
+        if args.model == "two_i" and not args.no_extra_configs:
+            cpu["mcmc_32chains"] = cpu_mcmc_baseline(m)
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     mh_flops, mh_flops_note = None, "skipped (--no-pmc, N>1 or no MCMC leg)"
     if world == 1 and not args.no_pmc and not args.mcmc_only:
