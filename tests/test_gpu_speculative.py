@@ -80,7 +80,11 @@ def test_rk4_speculative_state0_parameter_vs_c_restatement():
     kw = dict(nits=nits, burnin=10, walk_mask=walk, init_param=init_param, rng="replay", replay=(dz, u))
     eng = m.engine()
     spec = _np(eng.mh_run(theta, y0, speculate=4, **kw))
-    _equal(spec, _np(eng.mh_run(theta, y0, **kw)))
+    seq = _np(eng.mh_run(theta, y0, **kw))
+    _equal(spec, seq)
+    # depth 9: the one-wave-per-chain resolve (LDS tree), linked state included
+    _equal(_np(eng.mh_run(theta, y0, speculate="auto", **kw)), seq)
+    assert eng.last_mh_depth() == 9
     ref = rk_ref.mh_run(m.fit_problem(), theta, y0, nits, 10, walk, init_param=init_param, rng="replay",
                         replay=(dz, u))
     np.testing.assert_allclose(spec["samples"], ref["samples"], rtol=1e-11)
