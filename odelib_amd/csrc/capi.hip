@@ -355,10 +355,15 @@ __global__ void __launch_bounds__(256) k_np_draws(const oe::NpDrawArgs d) {
   if (w < d.W) oe::np_draw_lane(d, w);
 }
 
-// MH proposal draws (philox mode), one lane per walker; see oe::philox_draws
+// MH proposal draws (philox mode), one lane per (walker, iteration) of the chunk: counter-
+// based, so every draw is independent of the others (a few chains no longer draw their
+// iterations one after another); see oe::philox_draw_iteration
 __global__ void __launch_bounds__(256) k_philox_draws(const oe::DrawArgs d) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w < d.W) oe::philox_draws(d, w);
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n_it = d.it1 - d.it0;
+  if (g >= d.W * n_it) return;
+  const int64_t k = g / d.W;
+  oe::philox_draw_iteration(d, g - k * d.W, d.it0 + (int)k);
 }
 
 // k_mh_tree's resolution: one lane per chain walks its tree with k_mh's accept test and
@@ -1107,7 +1112,8 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       d.it0 = m.it0;
       d.it1 = m.it1;
       m.draw_it0 = it0;
-      hipLaunchKernelGGL(k_philox_draws, grid, block, 0, c->stream, d);
+      hipLaunchKernelGGL(k_philox_draws, dim3((unsigned)((W * (d.it1 - d.it0) + kBlock - 1) / kBlock)), block, 0,
+                         c->stream, d);
       OE_HIP(c, hipGetLastError());
     } else if (numpy) {
       nd.it0 = m.it0;

@@ -1099,10 +1099,10 @@ struct DrawArgs {
   double* u;   // [it1 - it0][W]
 };
 
-__device__ __forceinline__ void philox_draws(const DrawArgs d, int64_t w) {
+__device__ __forceinline__ void philox_draw_iteration(const DrawArgs d, int64_t w, int it) {
   const uint64_t gid = (uint64_t)(d.walker_offset + w);
   const int64_t W = d.W;
-  for (int it = d.it0; it < d.it1; ++it) {
+  {
     double* dz = d.dz + (int64_t)(it - d.it0) * d.P * W + w;
     for (int j = 0; j < d.P; j += 2) {
       const U4 r = philox4x32_10(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)it, (uint32_t)(j >> 1)},
