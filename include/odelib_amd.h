@@ -63,12 +63,17 @@ enum {
   OE_METHOD_DOPRI5 = 1, /* Dormand–Prince 5(4), wavefront-shared step, max-norm error,
                            dense output onto the times grid */
   OE_METHOD_AUTO = 2,   /* odeint's LSODA behaviour (Framework.py:656): DOPRI5 with a per-walker
-                           stiffness test; stiff or over-budget walkers are integrated again by
-                           the Rosenbrock method (status bit OE_STATUS_STIFF).  n_states <= 32
-                           (above 8 the Jacobian and LU factors live in private memory) */
-  OE_METHOD_ROSENBROCK = 3 /* stiffly accurate Rosenbrock 4(3) (RODAS) for every walker, exact
+                           stiffness test; a stiff or over-budget walker continues from that point
+                           with BDF (n_states <= 8), or is integrated again from t0 by the
+                           Rosenbrock method (9..32 states; the Jacobian and LU factors then live
+                           in private memory or one wave per walker).  Status bit OE_STATUS_STIFF */
+  OE_METHOD_ROSENBROCK = 3, /* stiffly accurate Rosenbrock 4(3) (RODAS) for every walker, exact
                               Jacobian by dual numbers, continuous extension onto the output
                               times.  n_states <= 32 */
+  OE_METHOD_BDF = 4      /* LSODA's stiff branch for every walker: variable-order (1..5) BDF in
+                            scipy's fixed-leading-coefficient form, max norm, modified Newton on an
+                            exact (dual-number) Jacobian; walkers share the step size and order per
+                            wave.  n_states <= 8 */
 };
 
 /* built-in right-hand sides (demo notebook models + synthetic chain) */
@@ -85,7 +90,7 @@ enum {
   OE_STATUS_NONFINITE = 1, /* a state became NaN/inf */
   OE_STATUS_NEGATIVE = 2,  /* a state went negative at an output time */
   OE_STATUS_MAXSTEP = 4,   /* step budget / step underflow: walker abandoned (NaN output) */
-  OE_STATUS_STIFF = 8,     /* OE_METHOD_AUTO: the walker was integrated by the stiff method */
+  OE_STATUS_STIFF = 8,     /* OE_METHOD_AUTO: the walker was handed to the stiff method */
   OE_STATUS_INTERNAL = 16  /* oe_mh_run: an internal integrity check failed; the chain stopped storing */
 };
 

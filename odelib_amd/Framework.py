@@ -7,9 +7,9 @@ and likelihood evaluation goes through ``libodelib_amd.so`` (``engine.Engine``).
 ODE callable is bound to a compiled device RHS by ``models.resolve_model``.
 
 Engine options (keyword-only, new): ``method`` ('auto' default — like odeint's LSODA:
-adaptive DOPRI5 with a per-walker stiffness test, stiff walkers redone by an L-stable
-Rosenbrock method; 'dopri5' by default for models wider than 8 states or where the
-stiff methods are unavailable — or 'dopri5', 'rosenbrock', 'rk4'), ``rtol``/``atol``
+adaptive DOPRI5 with a per-walker stiffness test, a stiff walker continues from that point
+with variable-order BDF; 'dopri5' by default for models wider than 8 states or where the
+stiff methods are unavailable — or 'dopri5', 'bdf', 'rosenbrock', 'rk4'), ``rtol``/``atol``
 (odeint defaults), ``rk4_substeps``, ``max_steps`` (odeint's mxstep), ``device`` (HIP
 device index; default: torch's current device when the engine is built),
 ``device_model`` (force a built-in RHS, or 'rtc'), ``device_rhs`` (C++ body of the RHS

@@ -19,7 +19,7 @@ OE_ABI_VERSION = 5
 OE_COMM_ID_BYTES = 128
 OE_OK = 0
 OE_ERR_ARG, OE_ERR_HIP, OE_ERR_STATE, OE_ERR_UNSUPPORTED, OE_ERR_NOMEM = -1, -2, -3, -4, -5
-OE_METHOD_RK4, OE_METHOD_DOPRI5, OE_METHOD_AUTO, OE_METHOD_ROSENBROCK = 0, 1, 2, 3
+OE_METHOD_RK4, OE_METHOD_DOPRI5, OE_METHOD_AUTO, OE_METHOD_ROSENBROCK, OE_METHOD_BDF = 0, 1, 2, 3, 4
 OE_MODEL_ZERO_I, OE_MODEL_ONE_I, OE_MODEL_TWO_I, OE_MODEL_CHAIN = 0, 1, 2, 3
 OE_MODEL_CUSTOM = 1000
 OE_STATUS_NONFINITE, OE_STATUS_NEGATIVE, OE_STATUS_MAXSTEP, OE_STATUS_STIFF, OE_STATUS_INTERNAL = 1, 2, 4, 8, 16

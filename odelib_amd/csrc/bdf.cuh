@@ -1,0 +1,478 @@
+// bdf.cuh — the BDF half of odeint's LSODA (Framework.py:656) on the device: variable-order
+// (1..5) backward differentiation formulas in the fixed-leading-coefficient backward-difference
+// form of scipy's BDF solver (the NDF scheme of Shampine & Reichelt with scipy's kappa table),
+// with the max norm LSODA uses and a modified Newton iteration: the LU factors of I − c·J are
+// kept across steps and rebuilt, from a fresh Jacobian, when the step size or the order
+// changes or Newton fails on factors from an earlier step.
+//
+// Why BDF and not the Rosenbrock method for the walkers 'auto' hands over:
+// LSODA switches to BDF, and on the draws that make the reference's fits expensive the two
+// differ by an order of magnitude.  A stiff component sitting on its quasi-steady state
+// (two_i's I1 at τ = 1e4: I1 ≈ φ·S·V/τ) drives a one-step Rosenbrock method into order
+// reduction — RODAS takes 3 688 steps at odeint's tolerances — while a multistep method's
+// error on it is the smooth (q+1)-th difference: 550-650 BDF steps, each ~2.4 RHS
+// evaluations and 1/5 of an LU factorisation (scipy's BDF: 546; LSODA: 734).
+//
+// Lockstep layout: the lanes that take part carry their OWN time t (a lane joins at its
+// DOPRI5 eviction point) but share the step size h and the order q (wave decisions from
+// wave-max norms), so every vector operation is uniform; only the dense output onto each
+// lane's own grid points diverges.  Steps may end past t_end (as LSODA's itask = 1
+// overshoot), the grid points come from the backward-difference interpolant.
+//
+// Everything is IEEE add/mul/fma/div plus frexp/ldexp, restated operation for operation in
+// oracle/rk_ref.c (bdf_group), so the kernel is bitwise testable.
+#pragma once
+
+namespace oe {
+namespace bdf {
+constexpr int kMaxQ = 5;
+constexpr int kRows = kMaxQ + 3;  // D[0..q+2]
+constexpr int kNewtonMaxIter = 4;
+constexpr int kBudget = 8;  // steps per output interval, in units of max_steps
+// scipy's BDF tables: gamma_q = Σ_{j<=q} 1/j, alpha_q = (1 − kappa_q)·gamma_q (1/alpha here),
+// error constants kappa_q·gamma_q + 1/(q+1), Newton-count safety 0.9·(2·4+1)/(2·4+n)
+__device__ const double kGamma[6] = {0.0, 1.0, 1.5, 1.8333333333333333, 2.083333333333333, 2.283333333333333};
+__device__ const double kInvAlpha[6] = {0.0, 0.8438818565400843, 0.6, 0.5039772202296456, 0.4608737397983678,
+                                        0.43795620437956206};
+__device__ const double kEc[6] = {1.0, 0.315, 0.16666666666666666, 0.09911666666666669, 0.11354166666666668,
+                                  0.16666666666666666};
+__device__ const double kSafety[5] = {0.0, 0.8999999999999999, 0.8099999999999999, 0.7363636363636363,
+                                      0.6749999999999999};
+__device__ const double kInvI[6] = {0.0, 1.0, 0.5, 0.3333333333333333, 0.25, 0.2};
+// U of scipy's change_D (R(q, 1)): U[m][j] = (−1)^m·C(j, m), exact integers
+__device__ const double kU[6][6] = {{1, 1, 1, 1, 1, 1},    {0, -1, -2, -3, -4, -5}, {0, 0, 1, 3, 6, 10},
+                                    {0, 0, 0, -1, -4, -10}, {0, 0, 0, 0, 1, 5},      {0, 0, 0, 0, 0, -1}};
+// x^(-1/q), q = 1..6: a linear start on m ∈ [0.5, 1), six Newton steps, the exponent part
+// 2^(−r/q)·2^(−Q) from a table (as inv_fifth_root)
+__device__ const double kIrS[7] = {0.0, -2.0, -0.8284271247461903, -0.5198420997897464, -0.37841423000544205,
+                                   -0.2973967099940702, -0.24492409661874603};
+__device__ const double kIrI[7] = {0.0, 3.0, 1.8284271247461903, 1.5198420997897464, 1.378414230005442,
+                                   1.2973967099940702, 1.244924096618746};
+__device__ const double kIrRq[7] = {0.0, 1.0, 0.5, 0.3333333333333333, 0.25, 0.2, 0.16666666666666666};
+__device__ const double kIrC[7][6] = {
+    {1.0, 0, 0, 0, 0, 0},
+    {1.0, 0, 0, 0, 0, 0},
+    {1.0, 0.7071067811865476, 0, 0, 0, 0},
+    {1.0, 0.7937005259840998, 0.6299605249474366, 0, 0, 0},
+    {1.0, 0.8408964152537145, 0.7071067811865476, 0.5946035575013605, 0, 0},
+    {1.0, 0.8705505632961241, 0.757858283255199, 0.6597539553864471, 0.5743491774985174, 0},
+    {1.0, 0.8908987181403393, 0.7937005259840998, 0.7071067811865476, 0.6299605249474366, 0.5612310241546865}};
+
+// x^(-1/q) for the step-size factors (x ≤ 0 → +inf: a zero error norm leaves the factor to
+// its clamp; +inf → 0).  q is wave-uniform at every call.
+__device__ __forceinline__ double inv_root(double x, int q) {
+  if (!(x > 0.0)) return __builtin_inf();
+  if (__builtin_isinf(x)) return 0.0;
+  int e;
+  const double m = frexp(x, &e);
+  int Q = e / q, r = e % q;
+  if (r < 0) { r += q; Q -= 1; }
+  const cptr<double> s = kconst(kIrS), ic = kconst(kIrI), rq = kconst(kIrRq);
+  double y = fma(s[q], m, ic[q]);
+  const double q1 = (double)(q + 1), rqq = rq[q];
+  for (int it = 0; it < 6; ++it) {
+    double yq = y;
+    for (int j = 1; j < q; ++j) yq = yq * y;
+    y = (y * fma(-m, yq, q1)) * rqq;
+  }
+  return ldexp(kconst(&kIrC[0][0])[q * 6 + r] * y, -Q);
+}
+
+// per-lane max norm of |c·v| against atol + rtol·|y| (argmax by cross-multiplication, one
+// division; non-finite → 1e30)
+template <int S>
+__device__ __forceinline__ double norm_max(double c, const double (&v)[S], const double (&y)[S], double rtol,
+                                           double atol) {
+  double num = 0.0, den = 1.0, nfe = 0.0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const double ae = fabs(c * v[s]);
+    const double sk = fma(rtol, fabs(y[s]), atol);
+    nfe = fma(ae, 0.0, nfe);
+    if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
+  }
+  double el = num / den;
+  if (!__builtin_isfinite(el) || __builtin_isnan(nfe)) el = 1e30;
+  return el;
+}
+
+// scipy's change_D for a step-size change by `factor` at order q, in two stages:
+// E = R(q, factor)^T D, then D = U^T E (the same product as (RU)^T D, U exact).  State by
+// state, so only one state's E is live (the R coefficients are recomputed per state: the
+// same values every time).
+template <int S>
+__device__ __forceinline__ void change_D(double (&D)[kRows][S], int q, double factor) {
+  const cptr<double> U = kconst(&kU[0][0]), inv_i = kconst(kInvI);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    double E[kMaxQ + 1];
+    E[0] = D[0][s];
+#pragma unroll
+    for (int m = 1; m <= kMaxQ; ++m) {
+      if (m > q) break;
+      double r = 1.0, e = D[0][s];
+#pragma unroll
+      for (int i = 1; i <= kMaxQ; ++i) {
+        if (i > q) break;
+        r = r * (((double)(i - 1) - factor * (double)m) * inv_i[i]);
+        e = fma(r, D[i][s], e);
+      }
+      E[m] = e;
+    }
+#pragma unroll
+    for (int j = 0; j <= kMaxQ; ++j) {
+      if (j > q) break;
+      double acc = E[0];
+#pragma unroll
+      for (int m = 1; m <= kMaxQ; ++m) {
+        if (m > j) break;
+        acc = fma(U[m * 6 + j], E[m], acc);
+      }
+      D[j][s] = acc;
+    }
+  }
+}
+
+// row `j` (wave-uniform, runtime) of D without indexing the register array
+template <int S>
+__device__ __forceinline__ void row(const double (&D)[kRows][S], int j, double (&out)[S]) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) out[s] = 0.0;
+#pragma unroll
+  for (int r = 0; r < kRows; ++r)
+    if (r == j) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) out[s] = D[r][s];
+    }
+}
+}  // namespace bdf
+
+// Output of one lane at its own grid index i (trajectory row store + minimum + observations):
+// per-lane addresses, so plain stores/loads instead of the uniform buffer descriptors.
+// Without a trajectory only observed grid points are emitted (as the DOPRI5 pass does).
+template <int S, bool TRAJ, bool NT>
+__device__ __forceinline__ void emit_lane(const DevProblem& pb, int i, const double (&y)[S], double* traj, int64_t W,
+                                          int64_t w, bool active, int& k, Acc& a) {
+  const Obs* obs = pb.obs;
+  const bool observed = k < pb.n_obs && obs[k].tidx == i;
+  if (!TRAJ && !observed) return;
+  track_min<S>(y, a);
+  if constexpr (TRAJ) {
+    if (active) {
+      double* row = traj + (int64_t)i * S * W + w;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if constexpr (NT) __builtin_nontemporal_store(y[s], row + (int64_t)s * W);
+        else row[(int64_t)s * W] = y[s];
+      }
+    }
+  }
+  if (!observed) return;
+  check_finite(y, a);
+  while (k < pb.n_obs && obs[k].tidx == i) {
+    const uint64_t mask = obs[k].mask;
+    const double O = obs[k].O, two_s2 = obs[k].two_s2, O_lin = obs[k].O_lin;
+    double c = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      if ((mask >> s) & 1ull) c = c + y[s];
+    const double d = O - oe_log(c);
+    const double term = (d * d) / two_s2;
+    if (__builtin_isfinite(term)) { a.chi += term; a.nvalid += 1; }
+    const double r = c - O_lin;
+    const double r2 = r * r;
+    if (!__builtin_isnan(r2)) a.ssres += r2;
+    ++k;
+  }
+}
+
+// The per-lane state of the BDF pass and the wave-shared controls.
+template <int S>
+struct BdfState {
+  double D[bdf::kRows][S];  // backward differences (scipy's D)
+  double lu[S][S], dinv[S]; // LU of I − c·J (J evaluated when the factors are built)
+  int piv[S];
+  double t;                 // this lane's time
+  int i, k, nst;            // next grid index, next observation, steps since the last grid point
+  bool live;
+  // wave-uniform
+  double h;
+  int order, neq;
+  bool lu_ok, fresh, any_swap;  // factors valid; built in this step (from this step's Jacobian)
+};
+
+// LU factors of I − c·J(t, y) for the lanes taking part
+template <class M, int PMAX>
+__device__ __forceinline__ void bdf_factor(BdfState<M::S>& st, double c, const double (&y)[M::S], double t,
+                                           const double (&p)[PMAX]) {
+  constexpr int S = M::S;
+  double f[S], ft[S];
+  jac_eval<M, PMAX>(y, t, p, f, st.lu, ft);
+#pragma unroll
+  for (int r = 0; r < S; ++r)
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      const double av = c * st.lu[r][q];
+      st.lu[r][q] = (r == q) ? 1.0 - av : -av;
+    }
+  st.any_swap = ros::lu_factor<S>(st.lu, st.piv, st.dinv);
+}
+
+// One step attempt at order Q (compile-time, so the difference rows are fixed registers and
+// the loops over them are straight-line code).
+template <class M, int PMAX, bool TRAJ, bool NT, int Q>
+__device__ __forceinline__ void bdf_step(const DevProblem& pb, BdfState<M::S>& st, double (&y)[M::S],
+                                         const double (&p)[PMAX], double* traj, int64_t W, int64_t w, bool active,
+                                         Acc& a) {
+  using namespace bdf;
+  constexpr int S = M::S;
+  const double rtol = pb.rtol, atol = pb.atol, ntol = pb.newton_tol;
+  const cptr<double> gam = kconst(kGamma);
+  const double ialpha = kconst(kInvAlpha)[Q];
+  const double h = st.h;
+  const double c = h * ialpha;
+  double yp[S], psi[S], rs[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    double v = st.D[0][s], ps = 0.0;
+#pragma unroll
+    for (int j = 1; j <= Q; ++j) {
+      v = v + st.D[j][s];
+      ps = fma(gam[j], st.D[j][s], ps);
+    }
+    yp[s] = v;
+    psi[s] = ps * ialpha;
+    rs[s] = 1.0 / fma(rtol, fabs(v), atol);
+  }
+  double yn[S], d[S];
+  bool bad = false;
+  int niter = 0;
+  if (!st.lu_ok) {  // factors for this step size and order, Jacobian at the current state
+    double y0[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) y0[s] = st.D[0][s];
+    bdf_factor<M, PMAX>(st, c, y0, st.t, p);
+    st.lu_ok = true;
+    st.fresh = true;
+  }
+  for (;;) {  // Newton; once more on factors from this step's predictor if it fails on older ones
+#pragma unroll
+    for (int s = 0; s < S; ++s) { yn[s] = yp[s]; d[s] = 0.0; }
+    bool conv = false, fail = false;
+    double dold = 0.0;
+    niter = 0;
+    for (int kk = 0; kk < kNewtonMaxIter; ++kk) {
+      const bool act = st.live && !conv && !fail;
+      if (__ballot(act) == 0ull) break;
+      niter = kk + 1;
+      if (act) {
+        double f[S], dy[S], nf = 0.0;
+        M::rhs(yn, st.t + h, p, f);
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          nf = fma(f[s], 0.0, nf);
+          dy[s] = (c * f[s] - psi[s]) - d[s];
+        }
+        if (__builtin_isnan(nf)) {
+          fail = true;
+        } else {
+          ros::lu_solve<S>(st.lu, st.piv, st.dinv, st.any_swap, dy);
+          double dn = 0.0;
+#pragma unroll
+          for (int s = 0; s < S; ++s) dn = fmax(dn, fabs(dy[s]) * rs[s]);
+          double rate = 0.0;
+          bool ok = true;
+          if (kk > 0) {
+            rate = dn / dold;
+            const double pw = (kk == 1) ? (rate * rate) * rate : (kk == 2) ? rate * rate : rate;
+            if (!(rate < 1.0) || pw / (1.0 - rate) * dn > ntol) { fail = true; ok = false; }
+          }
+          if (ok) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+              yn[s] = yn[s] + dy[s];
+              d[s] = d[s] + dy[s];
+            }
+            if (dn == 0.0 || (kk > 0 && rate / (1.0 - rate) * dn < ntol)) conv = true;
+            dold = dn;
+          }
+        }
+      }
+    }
+    bad = __ballot(st.live && !conv) != 0ull;
+    if (!bad || st.fresh) break;
+    bdf_factor<M, PMAX>(st, c, yp, st.t + h, p);
+    st.fresh = true;
+  }
+  if (bad) {
+    st.h = h * 0.5;
+    change_D<S>(st.D, Q, 0.5);
+    st.neq = 0;
+    st.lu_ok = false;
+    return;
+  }
+  const double safety = kconst(kSafety)[niter];
+  const cptr<double> ec = kconst(kEc);
+  const double el = st.live ? norm_max<S>(ec[Q], d, yn, rtol, atol) : 0.0;
+  const double en = wave_max(el);
+  if (en > 1.0) {
+    const double factor = fmax(0.2, safety * inv_root(en, Q + 1));
+    st.h = h * factor;
+    change_D<S>(st.D, Q, factor);
+    st.neq = 0;
+    return;
+  }
+  // accepted: differences, this lane's grid points, lanes that reach t_end leave
+  ++st.neq;
+  st.fresh = false;
+  const bool select = st.neq >= Q + 1;  // wave-uniform: order and step selection after this step
+  double em_l = 0.0, ep_l = 0.0;
+  bool voter = false;
+  if (st.live) {
+    const double tn = st.t + h;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      st.D[Q + 2][s] = d[s] - st.D[Q + 1][s];
+      st.D[Q + 1][s] = d[s];
+    }
+#pragma unroll
+    for (int j = Q; j >= 0; --j)
+#pragma unroll
+      for (int s = 0; s < S; ++s) st.D[j][s] = st.D[j][s] + st.D[j + 1][s];
+    ++st.nst;
+    double yo[S];
+    const double* times = pb.times;
+    while (st.i < pb.T && times[st.i] <= tn) {
+      const double ti = times[st.i];
+      double prod = 1.0;
+#pragma unroll
+      for (int s = 0; s < S; ++s) yo[s] = st.D[0][s];
+#pragma unroll
+      for (int j = 1; j <= Q; ++j) {
+        const double x = (ti - (tn - (double)(j - 1) * h)) / ((double)j * h);
+        prod = prod * x;
+#pragma unroll
+        for (int s = 0; s < S; ++s) yo[s] = fma(st.D[j][s], prod, yo[s]);
+      }
+      emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, a);
+      ++st.i;
+      st.nst = 0;
+    }
+    st.t = tn;
+    if (st.i >= pb.T) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) y[s] = yo[s];
+      st.live = false;
+    } else if (select) {
+      voter = true;
+      if constexpr (Q > 1) em_l = norm_max<S>(ec[Q - 1], st.D[Q], yn, rtol, atol);
+      if constexpr (Q < kMaxQ) ep_l = norm_max<S>(ec[Q + 1], st.D[Q + 2], yn, rtol, atol);
+    }
+  }
+  if (select && __ballot(voter) != 0ull) {
+    const double em = wave_max(em_l), ep = wave_max(ep_l);
+    const double fm = (Q > 1) ? inv_root(em, Q) : 0.0;
+    const double fe = inv_root(en, Q + 1);
+    const double fp = (Q < kMaxQ) ? inv_root(ep, Q + 2) : 0.0;
+    int dq = 0;
+    double fmx = fm;
+    if (fe > fmx) { fmx = fe; dq = 1; }
+    if (fp > fmx) { fmx = fp; dq = 2; }
+    const int q = Q + dq - 1;
+    const double factor = fmin(10.0, safety * fmx);
+    st.h = h * factor;
+    change_D<S>(st.D, q, factor);
+    st.order = q;
+    st.neq = 0;
+    st.lu_ok = false;
+  }
+}
+
+// BDF integration of the lanes with `part` set from their own (t, y, grid index i,
+// observation index k) with their accumulators as they are; the others sit out (no vote,
+// no output).  y is the final state (the last grid point's) on return.
+template <class M, int PMAX, bool TRAJ, bool NT>
+__device__ __forceinline__ void integrate_bdf(const DevProblem& pb, double (&y)[M::S], double t, int i, int k,
+                                              const double (&p)[PMAX], double* traj, int64_t W, int64_t w,
+                                              bool active, bool part, Acc& a) {
+  using namespace bdf;
+  constexpr int S = M::S;
+  const cptr<double> ctimes = kconst(pb.times);
+  const double tend = ctimes[pb.T - 1], t0 = ctimes[0];
+  const double rtol = pb.rtol, atol = pb.atol;
+  const int budget = kBudget * pb.max_steps;
+  BdfState<S> st;
+  st.live = part;
+  st.t = t;
+  st.i = i;
+  st.k = k;
+  st.nst = 0;
+  {
+    double f[S];
+    M::rhs(y, t, p, f);
+    // initial step: HINIT for order 1 (max norm), wave minimum over the lanes taking part
+    double d0 = 0.0, d1v = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double sk = atol + rtol * fabs(y[s]);
+      d0 = fmax(d0, fabs(y[s]) / sk);
+      d1v = fmax(d1v, fabs(f[s]) / sk);
+    }
+    const double rest = tend - t;
+    double h0 = (d0 <= 1e-5 || d1v <= 1e-5) ? 1e-6 : 0.01 * (d0 / d1v);
+    h0 = fmin(h0, rest);
+    double yt[S], f1[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) yt[s] = fma(h0, f[s], y[s]);
+    M::rhs(yt, t + h0, p, f1);
+    double d2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double sk = atol + rtol * fabs(y[s]);
+      d2 = fmax(d2, fabs(f1[s] - f[s]) / sk);
+    }
+    d2 = d2 / h0;
+    const double dm = fmax(d1v, d2);
+    const double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : inv_root(dm / 0.01, 2);
+    double hl = fmin(100.0 * h0, h1);
+    if (!__builtin_isfinite(hl) || !(hl > 0.0)) hl = rest;
+    if (!st.live) hl = __builtin_inf();
+    st.h = wave_min(hl);
+#pragma unroll
+    for (int j = 0; j < kRows; ++j)
+#pragma unroll
+      for (int s = 0; s < S; ++s) st.D[j][s] = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) { st.D[0][s] = y[s]; st.D[1][s] = f[s] * st.h; }
+  }
+  const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
+  st.order = 1;
+  st.neq = 0;
+  st.lu_ok = false;
+  st.fresh = false;
+  st.any_swap = false;
+  while (__ballot(st.live) != 0ull) {
+    switch (st.order) {  // wave-uniform
+      case 1: bdf_step<M, PMAX, TRAJ, NT, 1>(pb, st, y, p, traj, W, w, active, a); break;
+      case 2: bdf_step<M, PMAX, TRAJ, NT, 2>(pb, st, y, p, traj, W, w, active, a); break;
+      case 3: bdf_step<M, PMAX, TRAJ, NT, 3>(pb, st, y, p, traj, W, w, active, a); break;
+      case 4: bdf_step<M, PMAX, TRAJ, NT, 4>(pb, st, y, p, traj, W, w, active, a); break;
+      default: bdf_step<M, PMAX, TRAJ, NT, 5>(pb, st, y, p, traj, W, w, active, a); break;
+    }
+    // budget: a lane that needs more than `budget` steps inside one output interval, or a
+    // step below hmin, is abandoned (MAXSTEP, NaN for the rest of its grid)
+    if (st.live && (st.nst >= budget || st.h < hmin)) {
+      st.live = false;
+      a.status |= ST_MAXSTEP;
+      double yo[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
+      for (; st.i < pb.T; ++st.i) emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, a);
+#pragma unroll
+      for (int s = 0; s < S; ++s) y[s] = yo[s];
+    }
+  }
+  if (part) check_finite(y, a);
+}
+
+}  // namespace oe

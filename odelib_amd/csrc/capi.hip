@@ -696,9 +696,11 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   for (int i = 1; i < p->n_times; ++i)
     if (!(p->times[i] > p->times[i - 1]))
       return fail(c, OE_ERR_ARG, "oe_problem_set: times must be strictly increasing");
-  if (p->method < OE_METHOD_RK4 || p->method > OE_METHOD_ROSENBROCK)
+  if (p->method < OE_METHOD_RK4 || p->method > OE_METHOD_BDF)
     return fail(c, OE_ERR_ARG, "oe_problem_set: unknown method");
-  if (p->method == OE_METHOD_AUTO || p->method == OE_METHOD_ROSENBROCK) {
+  if (p->method == OE_METHOD_BDF && e->S > kStiffRegS)
+    return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: bdf needs n_states <= " + std::to_string(kStiffRegS));
+  if (p->method == OE_METHOD_AUTO || p->method == OE_METHOD_ROSENBROCK || p->method == OE_METHOD_BDF) {
     if (cm) {  // a user RHS: its stiff kernels are compiled the first time they are asked for
       if (cm->rtc.stiff == 0) {
         std::string err;
@@ -783,6 +785,8 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   d.max_steps = p->max_steps;
   d.pnum = p->pnum;
   d.sstot = p->sstot;
+  // scipy's BDF Newton tolerance (oracle/rk_ref.c bdf_newton_tol: the same expression)
+  d.newton_tol = std::fmax(10.0 * 2.220446049250313e-16 / p->rtol, std::fmin(0.03, std::sqrt(p->rtol)));
   c->method = p->method;
   c->entry = e;
   c->has_problem = true;

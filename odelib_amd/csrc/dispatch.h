@@ -23,11 +23,12 @@ struct Entry {
   int32_t model_id;
   int32_t S;
   int32_t P;  // the model's own parameter count
-  // [method][traj][nt]; methods kAuto / kRosenbrock are null when S > kStiffMaxS
-  IntegrateLaunch integrate[4][2][2];
+  // [method][traj][nt]; methods kAuto / kRosenbrock are null when S > kStiffMaxS, kBdf when
+  // S > kStiffRegS
+  IntegrateLaunch integrate[kMethods][2][2];
   IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > OE_PIPE_MAX_S
-  MHLaunch mh[4];
-  MHTreeLaunch mh_tree[4];  // speculative MH rounds (k_mh_tree); the resolve kernel is shared
+  MHLaunch mh[kMethods];
+  MHTreeLaunch mh_tree[kMethods];  // speculative MH rounds (k_mh_tree); the resolve kernel is shared
   StiffWaveLaunch stiff_wave[2][2];  // [traj][nt]: S > kStiffRegS stiff redo, one wave per walker
   IntegrateLaunch dopri5_split[2][2];  // [traj][nt]: DOPRI5 with split_lanes lanes per walker (split.cuh)
   MHLaunch mh_split = nullptr;         // DOPRI5 Metropolis–Hastings, split_lanes lanes per walker
@@ -147,6 +148,7 @@ Entry make_entry(int32_t model_id) {
     fill_method<M, kAuto>(e);
     fill_method<M, kRosenbrock>(e);
   }
+  if constexpr (M::S <= kStiffRegS) fill_method<M, kBdf>(e);
   if constexpr (M::S > kStiffRegS && M::S <= kStiffMaxS) {
     e.stiff_wave[0][0] = launch_stiff_wave<M, false, false>;
     e.stiff_wave[0][1] = launch_stiff_wave<M, false, false>;

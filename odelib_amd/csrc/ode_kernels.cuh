@@ -53,13 +53,15 @@ struct DevProblem {
   int32_t max_steps;    // DOPRI5 steps per output interval
   int32_t pnum;         // AIC parameter count
   double sstot;         // R² denominator
+  double newton_tol;    // BDF Newton tolerance, max(10·eps/rtol, min(0.03, sqrt(rtol))) (host-computed)
 };
 
 enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8, ST_INTERNAL = 16 };
 
 // integrators (OE_METHOD_*): fixed-step RK4, DOPRI5, DOPRI5 with stiffness detection and
 // the Rosenbrock fallback for stiff / over-budget walkers (LSODA-like), Rosenbrock only
-enum : int { kRK4 = 0, kDOPRI5 = 1, kAuto = 2, kRosenbrock = 3 };
+enum : int { kRK4 = 0, kDOPRI5 = 1, kAuto = 2, kRosenbrock = 3, kBdf = 4 };
+constexpr int kMethods = 5;
 constexpr int kStiffRegS = 8;   // up to here the stiff methods factor the S x S matrix in registers,
 constexpr int kStiffMaxS = 32;  // above it in private memory (stiff.cuh); wider models: DOPRI5 only
 constexpr int kStiffTestSteps = 3;  // auto: stiffness test from the 3rd step within one output interval
@@ -70,6 +72,17 @@ constexpr int kStiffTestSteps = 3;  // auto: stiffness test from the 3rd step wi
 // at the stability limit ~1.1 us per step, the register RODAS redo 3-6.5 ms, so ~4000
 // steps; the wide-model in-kernel redo (MH, matrices in private memory) is ~10-20x slower.
 constexpr double kStiffSwitchSteps = 4000.0, kStiffSwitchStepsSlow = 40000.0;
+// auto with S <= kStiffRegS: an evicted lane continues from its eviction point with BDF
+// (bdf.cuh), which costs only the rest of the span, so the hand-over is cheap and taken
+// early: the test runs from the 2nd step inside an output interval while finishing would
+// take over kBdfSwitchSteps DOPRI5 steps, and a step counts as stiff at h·|λ| > 2.5 (the
+// stability-limited crawl sits at 3.0-3.7) or, while over kBdfSwitchLong steps remain, at
+// h·|λ| > 0.5 (accuracy-limited on a fast component: two_i τ = 1e3 takes DOPRI5 2 359
+// steps at h·|λ| ≈ 0.9, the hand-over 94 + 436 BDF).
+constexpr int kBdfTestSteps = 2;
+constexpr double kBdfSwitchSteps = 300.0, kBdfSwitchLong = 1500.0;
+constexpr double kBdfThr2 = 6.25, kBdfThrLong2 = 0.25;
+
 
 // per-lane accumulators of the fused likelihood
 struct Acc {
@@ -82,6 +95,17 @@ struct Acc {
 };
 
 __device__ __forceinline__ Acc acc_init() { return Acc{0.0, 0.0, 0.0, __builtin_inf(), 0, 0}; }
+
+// where 'auto' (S <= kStiffRegS) hands a lane to BDF: the state at the start of the step it
+// was evicted on (or after the step that exhausted the budget), the next grid and
+// observation indices, and the accumulators so far
+template <int S>
+struct Resume {
+  double y[S];
+  double t;
+  int32_t i, k;
+  Acc a;
+};
 
 __device__ __forceinline__ int32_t finish(const Acc& a) {
   int32_t st = a.status;
@@ -493,10 +517,13 @@ __device__ __forceinline__ double inv_fifth_root_uniform(double x, cptr<double> 
 // AUTO: Hairer's stiffness test on every accepted step (h·|λ| estimated from the last two
 // stages, ≥ 3.25 on 15 accepted steps in a row evicts the lane, as does the step
 // budget); returns whether this (active) lane was evicted, i.e. needs the stiff method.
-template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false, bool SLOW_REDO = false>
+// RESUME (auto, S <= kStiffRegS): an evicted lane is handed over to BDF — its state at the
+// eviction point goes to *rs and the return value says so — instead of being redone from t0.
+template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false, bool SLOW_REDO = false, bool RESUME = false>
 __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
-                                                 int64_t W, uint32_t off, bool active, Acc& a) {
+                                                 int64_t W, uint32_t off, bool active, Acc& a,
+                                                 Resume<M::S>* rs = nullptr) {
   using namespace dp;
   constexpr int S = M::S;
   int k = 0;
@@ -506,6 +533,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
   const double tend = times[pb.T - 1];
   const double rtol = pb.rtol, atol = pb.atol;
   bool dead = !active;  // dead lanes never enter the wave norm
+  bool handed = false;  // RESUME: this lane was handed over to BDF
   double t = t0;
   const Tab tb = load_tab<TRAJ && (M::S <= 8)>();
   double k1[S], k2[S], k3[S], k4[S], k5[S], k6[S], k7[S], yt[S], yn[S];
@@ -547,6 +575,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
   // lanes poisoned with NaN (no per-point select).  S > 8 sits at the register limit,
   // so it keeps the leaner form (same outputs and status bits).
   constexpr bool kLean = S > 8;
+  static_assert(!RESUME || (AUTO && !kLean), "the BDF hand-over is the register path's");
   int i = 1;
   double t_i = times[1];
   cptr<double> tnext = times + 2;  // &times[i + 1]
@@ -592,10 +621,11 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
     // that will test (the same wave-uniform gate, one step ahead of the ++nst below), so
     // the stage-6 input dies before k7 instead of living through the error norm — S more
     // doubles at the kernel's register peak (same values, same order: bit-identical)
-    constexpr double kSwitch = SLOW_REDO ? kStiffSwitchStepsSlow : kStiffSwitchSteps;
+    constexpr double kSwitch = RESUME ? kBdfSwitchSteps : SLOW_REDO ? kStiffSwitchStepsSlow : kStiffSwitchSteps;
+    constexpr int kTestSteps = RESUME ? kBdfTestSteps : kStiffTestSteps;
     double stden_early = 0.0;
     if constexpr (AUTO && kLean) {
-      if (nst + 1 >= kStiffTestSteps && (tend - t) > kSwitch * h) {
+      if (nst + 1 >= kTestSteps && (tend - t) > kSwitch * h) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           const double r = 1.0 / fma(rtol, max_abs_raw(y[s], yn[s]), atol);
@@ -637,8 +667,9 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
       // The test also runs only while the shared step is below (t_end - t)/kSwitch (the
       // cost gate above), so a mildly stiff wave that DOPRI5 finishes cheaper than the
       // Rosenbrock redo never pays for it.
-      if (AUTO && nst >= kStiffTestSteps && (tend - t) > kSwitch * h) {
+      if (AUTO && nst >= kTestSteps && (tend - t) > kSwitch * h) {
         double stnum = 0.0, stden = stden_early;
+        const double thr2 = !RESUME ? 10.5625 : ((tend - t) > kBdfSwitchLong * h) ? kBdfThrLong2 : kBdfThr2;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           const double r = 1.0 / fma(rtol, max_abs_raw(y[s], yn[s]), atol);
@@ -649,7 +680,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
             stden = fma(dy, dy, stden);
           }
         }
-        if (stden > 0.0 && (h * h) * stnum > 10.5625 * stden) {
+        if (stden > 0.0 && (h * h) * stnum > thr2 * stden) {
           n_nonstiff = 0;
           ++n_stiff;
         } else if (++n_nonstiff >= 6) {
@@ -657,6 +688,15 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
         }
         if (!dead && n_stiff >= 15) {  // hand the walker to the stiff method
           dead = true;
+          if constexpr (RESUME) {  // at the start of this step
+            handed = true;
+#pragma unroll
+            for (int s = 0; s < S; ++s) rs->y[s] = y[s];
+            rs->t = t;
+            rs->i = i;
+            rs->k = k;
+            rs->a = a;
+          }
 #pragma unroll
           for (int s = 0; s < S; ++s) { yn[s] = __builtin_nan(""); k7[s] = __builtin_nan(""); }
         }
@@ -776,7 +816,17 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
     if (i < pb.T && (nst >= pb.max_steps || h < hmin)) {  // (not after the last grid point)
       if (!dead && el >= 0.5 * err) {
         dead = true;
-        a.status |= ST_MAXSTEP;
+        if constexpr (RESUME) {  // handed over at its current state
+          handed = true;
+#pragma unroll
+          for (int s = 0; s < S; ++s) rs->y[s] = y[s];
+          rs->t = t;
+          rs->i = i;
+          rs->k = k;
+          rs->a = a;
+        } else {
+          a.status |= ST_MAXSTEP;
+        }
         // poison the lane: every later dense output (and the final state) is NaN
         if constexpr (!kLean) {
 #pragma unroll
@@ -799,11 +849,13 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
   if (dead && active) a.status |= ST_MAXSTEP;
   check_finite(y, a);
   if (kLean && dead) a.nf = __builtin_nan("");  // as if poisoned: final state non-finite
+  if constexpr (RESUME) return handed && active;
   return dead && active;
 }
 
 }  // namespace oe
 #include "stiff.cuh"
+#include "bdf.cuh"
 namespace oe {
 
 // WAVE_REDO (batched integrate of models wider than kStiffRegS): 'auto' only marks the
@@ -818,6 +870,33 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
     integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
   } else if constexpr (METHOD == kDOPRI5 || M::S > kStiffMaxS) {
     integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  } else if constexpr (METHOD == kBdf) {  // LSODA's BDF branch for every walker (S <= kStiffRegS)
+    static_assert(M::S <= kStiffRegS, "bdf: register path only");
+    int k = 0;
+    emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
+    integrate_bdf<M, PMAX, TRAJ, NT>(pb, y, kconst(pb.times)[0], 1, k, p, traj, W, w, active, active, a);
+  } else if constexpr (METHOD == kAuto && M::S <= kStiffRegS) {
+    // LSODA-like: DOPRI5 with the stiffness test; a lane it evicts (stiff, or over the step
+    // budget) continues from the eviction point with BDF (status bit ST_STIFF)
+    Resume<M::S> rs;  // defined for every lane (only handed lanes use it)
+#pragma unroll
+    for (int s = 0; s < M::S; ++s) rs.y[s] = y[s];
+    rs.t = 0.0;
+    rs.i = pb.T;
+    rs.k = 0;
+    rs.a = a;
+    const bool handed = integrate_dopri5<M, PMAX, TRAJ, NT, true, false, true>(pb, y, p, traj, W, off, active, a, &rs);
+    if (__ballot(handed) != 0ull) {  // wave-uniform
+      if (handed) {
+        a = rs.a;
+        a.status |= ST_STIFF;
+      }
+      integrate_bdf<M, PMAX, TRAJ, NT>(pb, rs.y, rs.t, rs.i, rs.k, p, traj, W, w, active, handed, a);
+      if (handed) {
+#pragma unroll
+        for (int s = 0; s < M::S; ++s) y[s] = rs.y[s];
+      }
+    }
   } else if constexpr (METHOD == kAuto && WAVE_REDO) {
     if (integrate_dopri5<M, PMAX, TRAJ, NT, true>(pb, y, p, traj, W, off, active, a)) a.status |= ST_STIFF;
   } else if constexpr (METHOD == kAuto) {
@@ -883,13 +962,16 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t G, int32_t c) {
 template <class M>
 constexpr int kPmax = M::P + (M::S < 4 ? M::S : 4);
 
-// S = 5 stiff methods: the DOPRI5 + RODAS kernel needs 256 VGPRs + 14-22 AGPRs (one wave
-// per SIMD); asking for two leaves 32-48 B of scratch and measured (262 144 walkers,
-// profiles/r02o_occ*): `auto` 1.25 vs 1.70 ms without trajectory, 2.09 vs 2.22 with,
-// `rosenbrock` 6.3 vs 8.3 ms.  S = 6..8 kernels sit at one wave per SIMD for DOPRI5 too.
+// S = 5 Rosenbrock: the RODAS kernel needs 256 VGPRs + 14-22 AGPRs (one wave per SIMD);
+// asking for two leaves 32-48 B of scratch and measured (262 144 walkers, profiles/r02o_occ*)
+// `rosenbrock` 6.3 vs 8.3 ms (the r02 DOPRI5 + RODAS `auto` kernel: 1.25 vs 1.70 ms without
+// trajectory).  The r04 `auto` (DOPRI5 + BDF hand-over) and `bdf` kernels need ~280 registers
+// even for S = 4 (the difference table, LU factors and Newton vectors of the BDF pass): at two
+// waves per SIMD they spill 250-400 B per lane, so they run at one (VGPRs + AGPRs, no scratch);
+// below 65 536 walkers (the MH and speculative-round ensembles) that is one wave per SIMD anyway.
 template <class M, int METHOD, bool TRAJ, bool NT>
 __global__ void __launch_bounds__(256)
-    __attribute__((amdgpu_waves_per_eu((METHOD >= kAuto && M::S == 5) ? 2 : 1)))
+    __attribute__((amdgpu_waves_per_eu((METHOD == kRosenbrock && M::S == 5) ? 2 : 1)))
     k_integrate(const DevProblem pb, const IntegrateArgs ia) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
@@ -1191,7 +1273,7 @@ __device__ __forceinline__ T* opaque(T* p) {
 // scratch, in the rare path).  S = 6..8 DOPRI5 MH kernels are at one wave per SIMD anyway.
 template <class M, int METHOD>
 __global__ void __launch_bounds__(256)
-    __attribute__((amdgpu_waves_per_eu((METHOD >= kAuto && M::S == 5) ? 2 : 1)))
+    __attribute__((amdgpu_waves_per_eu((METHOD == kRosenbrock && M::S == 5) ? 2 : 1)))
     k_mh(const DevProblem pb, const MHArgs ma) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
@@ -1354,7 +1436,7 @@ struct MHTreeArgs {
 
 template <class M, int METHOD>
 __global__ void __launch_bounds__(256)
-    __attribute__((amdgpu_waves_per_eu((METHOD >= kAuto && M::S == 5) ? 2 : 1)))
+    __attribute__((amdgpu_waves_per_eu((METHOD == kRosenbrock && M::S == 5) ? 2 : 1)))
     k_mh_tree(const DevProblem pb, const MHTreeArgs ta) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;

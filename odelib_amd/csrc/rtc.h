@@ -7,15 +7,15 @@
 namespace oe {
 
 // The kernels of one user RHS, built in two parts on demand: the explicit methods (RK4,
-// DOPRI5) when the model is compiled, the stiff ones (auto, Rosenbrock: the body
+// DOPRI5) when the model is compiled, the stiff ones (auto, Rosenbrock, BDF: the body
 // instantiated with dual numbers, plus the one-wave-per-walker kernel for S > 8) the first
 // time a problem asks for them.
 struct RtcModule {
   hipModule_t mod = nullptr;              // RK4 + DOPRI5
-  hipModule_t stiff_mod = nullptr;        // auto + Rosenbrock (+ k_stiff_wave)
-  hipFunction_t integrate[4][2][2] = {};  // [method][traj][nt]; the stiff methods null until built
-  hipFunction_t mh[4] = {};
-  hipFunction_t mh_tree[4] = {};          // speculative MH rounds (k_mh_tree)
+  hipModule_t stiff_mod = nullptr;        // auto + Rosenbrock + BDF (+ k_stiff_wave)
+  hipFunction_t integrate[5][2][2] = {};  // [method][traj][nt]; the stiff methods null until built
+  hipFunction_t mh[5] = {};
+  hipFunction_t mh_tree[5] = {};          // speculative MH rounds (k_mh_tree)
   hipFunction_t stiff_wave[2][2] = {};    // [traj][nt]: S > kStiffRegS with the stiff methods
   int stiff = 0;                          // 0: not built yet, 1: built, -1: unavailable (stiff_err)
   std::string stiff_err;

@@ -22,7 +22,7 @@
 
 namespace oe {
 
-static const char* kMethodName[4] = {"0", "1", "2", "3"};
+static const char* kMethodName[5] = {"0", "1", "2", "3", "4"};
 static const char* kBool[2] = {"false", "true"};
 
 std::string rtc_integrate_name(int method, int traj, int nt) {
@@ -37,6 +37,8 @@ std::string rtc_stiff_wave_name(int traj, int nt) {
 }
 static bool has_stiff_wave(int S, RtcPart part) { return part == kRtcStiff && S > kStiffRegS; }
 static int first_method(RtcPart part) { return part == kRtcStiff ? 2 : 0; }
+// the methods of a part: RK4 + DOPRI5; auto + Rosenbrock (+ BDF up to kStiffRegS states)
+static int end_method(int S, RtcPart part) { return part == kRtcStiff ? (S <= kStiffRegS ? 5 : 4) : 2; }
 
 std::string rtc_source(const std::string& body, int S, int P, RtcPart part) {
   std::string src;
@@ -50,7 +52,7 @@ std::string rtc_source(const std::string& body, int S, int P, RtcPart part) {
   src += "    (void)t;\n";
   src += body;
   src += "\n  }\n};\n";
-  for (int m = first_method(part); m < first_method(part) + 2; ++m) {
+  for (int m = first_method(part); m < end_method(S, part); ++m) {
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)
         src += "template __global__ void " + rtc_integrate_name(m, tr, nt) + "(const oe::DevProblem, const oe::IntegrateArgs);\n";
@@ -105,11 +107,11 @@ static int compile_program(const std::string& src, const char* arch, std::vector
 static std::vector<std::string> all_names(int S, RtcPart part) {
   std::vector<std::string> names;
   const int m0 = first_method(part);
-  for (int m = m0; m < m0 + 2; ++m)
+  for (int m = m0; m < end_method(S, part); ++m)
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_integrate_name(m, tr, nt));
-  for (int m = m0; m < m0 + 2; ++m) names.push_back(rtc_mh_name(m));
-  for (int m = m0; m < m0 + 2; ++m) names.push_back(rtc_mh_tree_name(m));
+  for (int m = m0; m < end_method(S, part); ++m) names.push_back(rtc_mh_name(m));
+  for (int m = m0; m < end_method(S, part); ++m) names.push_back(rtc_mh_tree_name(m));
   if (has_stiff_wave(S, part))
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_stiff_wave_name(tr, nt));
@@ -148,13 +150,13 @@ int rtc_build(const std::string& body, int S, int P, const char* arch, RtcPart p
     }
     return true;
   };
-  for (int m = m0; m < m0 + 2; ++m)
+  for (int m = m0; m < end_method(S, part); ++m)
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)
         if (!get(&out->integrate[m][tr][nt])) return -1;
-  for (int m = m0; m < m0 + 2; ++m)
+  for (int m = m0; m < end_method(S, part); ++m)
     if (!get(&out->mh[m])) return -1;
-  for (int m = m0; m < m0 + 2; ++m)
+  for (int m = m0; m < end_method(S, part); ++m)
     if (!get(&out->mh_tree[m])) return -1;
   if (has_stiff_wave(S, part))
     for (int tr = 0; tr < 2; ++tr)

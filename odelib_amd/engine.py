@@ -22,7 +22,7 @@ import numpy as np
 from . import _native as N
 
 METHODS = {"rk4": N.OE_METHOD_RK4, "dopri5": N.OE_METHOD_DOPRI5, "auto": N.OE_METHOD_AUTO,
-           "rosenbrock": N.OE_METHOD_ROSENBROCK}
+           "rosenbrock": N.OE_METHOD_ROSENBROCK, "bdf": N.OE_METHOD_BDF}
 ODEINT_TOL = 1.49012e-8  # scipy.integrate.odeint default rtol/atol (Framework.py:656)
 # widest model for which a defaulted method 'auto' stays 'auto' (the register-resident
 # stiff path, ode_kernels.cuh kStiffRegS); wider models default to 'dopri5'

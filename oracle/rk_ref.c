@@ -29,12 +29,18 @@
 #include <string.h>
 
 #define LANES 64
+#ifndef BDF_SWITCH_LONG
+#define BDF_SWITCH_LONG 1500.0
+#endif
+#ifndef BDF_THR_LONG2
+#define BDF_THR_LONG2 0.25
+#endif
 #define MAXS 64
 #define MAXP 80
 
 enum { M_ZERO_I = 0, M_ONE_I = 1, M_TWO_I = 2, M_CHAIN = 3 };
 enum { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8 };
-enum { METHOD_RK4 = 0, METHOD_DOPRI5 = 1, METHOD_AUTO = 2, METHOD_ROSENBROCK = 3 };
+enum { METHOD_RK4 = 0, METHOD_DOPRI5 = 1, METHOD_AUTO = 2, METHOD_ROSENBROCK = 3, METHOD_BDF = 4 };
 
 typedef struct {
   int model, S, P, T;
@@ -49,6 +55,7 @@ typedef struct {
   double rtol, atol;
   int wave_redo; /* batched integrate of S > 8: stiff walkers redone one per group
                     (odelib_amd/csrc/stiff_wave.cuh: one wave per walker, own step size) */
+  double newton_tol; /* BDF: Newton convergence tolerance (from rtol, as scipy's BDF) */
   int split;     /* DOPRI5 with a walker over `split` lanes (odelib_amd/csrc/split.cuh): groups of
                     64/split walkers share a step size; a walker's error norm is the argmax over
                     each lane's states, combined in a tree of lanes (lower lane kept on ties) */
@@ -193,7 +200,10 @@ typedef struct {
   int kobs;
   int n_stiff, n_nonstiff; /* auto: consecutive stiff / non-stiff accepted steps */
   int part;                /* rosenbrock: lane takes part in the stiff integration */
-  double y0c[MAXS];        /* auto: initial state, for the restart */
+  double y0c[MAXS];        /* auto: initial state, for the restart; S <= 8: the hand-over state */
+  double t_ev;             /* auto, S <= 8: time of the hand-over to BDF */
+  int i_ev, k_ev;          /* ... and the next grid / observation index there */
+  int handed;              /* auto, S <= 8: the DOPRI5 pass handed this lane to BDF */
 } Lane;
 
 /* x^(-1/5), same operations as ode_kernels.cuh inv_fifth_root (bit-identical) */
@@ -217,11 +227,18 @@ double ref_inv_fifth_root(double x) { return inv_fifth_root(x); }
 
 /* DOPRI5 step statistics over all groups since the last reset (analysis only:
    tools/dopri5_steps.py) -- accepted and rejected lockstep steps, groups integrated */
-static long long g_dp_stats[3];
+static long long g_dp_stats[3], g_ros_stats[2];
 void ref_dopri5_stats(long long* out, int reset) {
   for (int j = 0; j < 3; ++j) {
     out[j] = g_dp_stats[j];
     if (reset) g_dp_stats[j] = 0;
+  }
+}
+/* Rosenbrock lockstep steps (accepted + rejected) and groups since the last reset (analysis only) */
+void ref_rosenbrock_stats(long long* out, int reset) {
+  for (int j = 0; j < 2; ++j) {
+    out[j] = g_ros_stats[j];
+    if (reset) g_ros_stats[j] = 0;
   }
 }
 
@@ -238,8 +255,12 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
   const int S = pb->S;
   const double t0 = pb->times[0], tend = pb->times[pb->T - 1];
   const double rtol = pb->rtol, atol = pb->atol;
+  /* auto with S <= 8 (ode_kernels.cuh kBdfMaxS): evicted lanes are handed to BDF at the
+     eviction point (no NaN poisoning, no further output from this pass) */
+  const int resume = autom && S <= 8;
   for (int l = 0; l < nl; ++l) {
     L[l].dead = !L[l].active;
+    L[l].handed = 0;
     L[l].kobs = 0;
     L[l].n_stiff = L[l].n_nonstiff = 0;
     emit(pb, 0, L[l].y, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
@@ -337,8 +358,13 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     if (err <= 1.0) {
       /* cost gate (ode_kernels.cuh kStiffSwitchSteps / kStiffSwitchStepsSlow): tested only
          while the shared step is below (tend - t)/N */
-      const double nsw = (S <= 8 || pb->wave_redo) ? 4000.0 : 40000.0;
-      if (autom && nst >= 3 && (tend - t) > nsw * h) { /* ode_kernels.cuh kStiffTestSteps */
+      const double nsw = resume ? 300.0 : (S <= 8 || pb->wave_redo) ? 4000.0 : 40000.0;
+      const int ntest = resume ? 2 : 3; /* ode_kernels.cuh kBdfTestSteps / kStiffTestSteps */
+      /* (h|lambda|)^2 above which a tested step counts as stiff: resume (S <= 8) 2.5^2 at the
+         stability limit, or 0.5^2 while finishing at this step would take over 1500 more steps
+         (accuracy-limited on a fast component, where BDF takes far fewer); otherwise 3.25^2 */
+      const double thr2 = !resume ? 10.5625 : ((tend - t) > BDF_SWITCH_LONG * h) ? BDF_THR_LONG2 : 6.25;
+      if (autom && nst >= ntest && (tend - t) > nsw * h) { /* ode_kernels.cuh kBdfSwitchSteps */
         for (int l = 0; l < nl; ++l) {
           Lane* q = &L[l];
           /* components weighted by 1/(atol + rtol·max(|y|,|ynew|)), the error scale */
@@ -349,7 +375,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
             stnum = fma(dk, dk, stnum);
             stden = fma(dy, dy, stden);
           }
-          if (stden > 0.0 && (h * h) * stnum > 10.5625 * stden) {
+          if (stden > 0.0 && (h * h) * stnum > thr2 * stden) {
             q->n_nonstiff = 0;
             ++q->n_stiff;
           } else if (++q->n_nonstiff >= 6) {
@@ -357,6 +383,13 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
           }
           if (!q->dead && q->n_stiff >= 15) {
             q->dead = 1;
+            if (resume) { /* hand over at the start of this step: (t, y), next grid index i */
+              q->handed = 1;
+              memcpy(q->y0c, q->y, sizeof(double) * S);
+              q->t_ev = t;
+              q->i_ev = i;
+              q->k_ev = q->kobs;
+            }
             for (int s = 0; s < S; ++s) q->yn[s] = q->k7[s] = NAN;
           }
         }
@@ -367,7 +400,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
       while (i < pb->T && pb->times[i] <= tn) {
         for (int l = 0; l < nl; ++l) {
           Lane* q = &L[l];
-          if (!needs_emit(pb, traj != NULL, i, q->kobs)) continue;
+          if (q->handed || !needs_emit(pb, traj != NULL, i, q->kobs)) continue;
           double yo[MAXS];
           double ti = pb->times[i];
           if (ti == tn) {
@@ -409,6 +442,14 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
       for (int l = 0; l < nl; ++l)
         if (!L[l].dead && L[l].el >= 0.5 * err) {
           L[l].dead = 1;
+          if (resume) { /* handed to BDF at the current state */
+            L[l].handed = 1;
+            memcpy(L[l].y0c, L[l].y, sizeof(double) * S);
+            L[l].t_ev = t;
+            L[l].i_ev = i;
+            L[l].k_ev = L[l].kobs;
+            continue;
+          }
           L[l].a.status |= ST_MAXSTEP;
           for (int s = 0; s < S; ++s) L[l].y[s] = L[l].k1[s] = NAN; /* evicted: NaN from here on */
         }
@@ -420,7 +461,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
         for (int s = 0; s < S; ++s) yo[s] = NAN;
         for (; i < pb->T; ++i)
           for (int l = 0; l < nl; ++l)
-            if (needs_emit(pb, traj != NULL, i, L[l].kobs))
+            if (!L[l].handed && needs_emit(pb, traj != NULL, i, L[l].kobs))
               emit(pb, i, yo, L[l].active ? traj : NULL, W, L[l].w, &L[l].kobs, &L[l].a);
         break;
       }
@@ -428,6 +469,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     }
   }
   for (int l = 0; l < nl; ++l) {
+    if (L[l].handed) continue; /* its output and status come from the BDF pass */
     if (L[l].dead && L[l].active) L[l].a.status |= ST_MAXSTEP;
     check_finite(S, L[l].y, &L[l].a);
   }
@@ -663,7 +705,9 @@ static void rodas_group(const Prob* pb, Lane* L, int nl, const double* p, double
   const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
   const int budget = 8 * pb->max_steps; /* stiff.cuh kRosBudget */
   int i = 1, nst = 0, last_rej = 0;
+  long long n_ros = 0;
   while (i < pb->T) {
+    ++n_ros;
     int last = 0;
     if (t + h >= tend) { h = tend - t; last = 1; }
     const double rh = 1.0 / h, gh = rh * r_inv_gam;
@@ -787,11 +831,399 @@ static void rodas_group(const Prob* pb, Lane* L, int nl, const double* p, double
   }
   for (int l = 0; l < nl; ++l)
     if (L[l].part) check_finite(S, L[l].y, &L[l].a);
+#pragma omp atomic
+  g_ros_stats[0] += n_ros;
+#pragma omp atomic
+  g_ros_stats[1] += 1;
 }
 
-/* 'auto': DOPRI5 with the stiffness test, then the evicted walkers again from t0 by RODAS */
+
+/* ---- BDF: variable order 1..5 in the fixed-leading-coefficient backward-difference form of
+   scipy's BDF solver (Shampine & Reichelt's NDF family with kappa = 0 at orders 1..5 replaced
+   by scipy's kappa table), for lanes with their OWN time and a shared step size and order
+   (bdf.cuh).  Max norm (as LSODA), modified Newton: the LU factors of I - c J are kept across
+   steps and rebuilt from a fresh Jacobian -- at the current state when the step size or the
+   order changed, at the predictor when Newton fails on factors from an earlier step.  Steps may end past t_end; grid points come from the
+   backward-difference interpolant.  'auto' with S <= 8 hands a lane here at its DOPRI5
+   eviction point; method 'bdf' starts every lane at t0. ---- */
+#define BDF_MAXQ 5
+#define BDF_NEWTON_MAXITER 4
+#define BDF_BUDGET 8 /* steps per output interval, in units of max_steps */
+static const double bdf_gamma[6] = {0.0, 1.0, 1.5, 1.8333333333333333, 2.083333333333333, 2.283333333333333};
+static const double bdf_inv_alpha[6] = {0.0, 0.8438818565400843, 0.6, 0.5039772202296456, 0.4608737397983678,
+                                        0.43795620437956206};
+static const double bdf_ec[6] = {1.0, 0.315, 0.16666666666666666, 0.09911666666666669, 0.11354166666666668,
+                                 0.16666666666666666};
+static const double bdf_safety[5] = {0.0, 0.8999999999999999, 0.8099999999999999, 0.7363636363636363,
+                                     0.6749999999999999};
+static const double bdf_inv_i[6] = {0.0, 1.0, 0.5, 0.3333333333333333, 0.25, 0.2};
+
+static double bdf_newton_tol(double rtol) { return fmax(10.0 * 2.220446049250313e-16 / rtol, fmin(0.03, sqrt(rtol))); }
+
+/* x^(-1/q), q = 1..6, for the step-size factors: frexp/ldexp and IEEE mul/fma only (bit-identical
+   to bdf.cuh inv_root); x <= 0 (a zero error norm) -> +inf, x = +inf -> 0 */
+static const double ir_s[7] = {0.0, -2.0, -0.8284271247461903, -0.5198420997897464, -0.37841423000544205,
+                               -0.2973967099940702, -0.24492409661874603};
+static const double ir_i[7] = {0.0, 3.0, 1.8284271247461903, 1.5198420997897464, 1.378414230005442,
+                               1.2973967099940702, 1.244924096618746};
+static const double ir_rq[7] = {0.0, 1.0, 0.5, 0.3333333333333333, 0.25, 0.2, 0.16666666666666666};
+static const double ir_c[7][6] = {
+    {1.0, 0, 0, 0, 0, 0},
+    {1.0, 0, 0, 0, 0, 0},
+    {1.0, 0.7071067811865476, 0, 0, 0, 0},
+    {1.0, 0.7937005259840998, 0.6299605249474366, 0, 0, 0},
+    {1.0, 0.8408964152537145, 0.7071067811865476, 0.5946035575013605, 0, 0},
+    {1.0, 0.8705505632961241, 0.757858283255199, 0.6597539553864471, 0.5743491774985174, 0},
+    {1.0, 0.8908987181403393, 0.7937005259840998, 0.7071067811865476, 0.6299605249474366, 0.5612310241546865}};
+static double inv_root(double x, int q) {
+  if (!(x > 0.0)) return INFINITY;
+  if (isinf(x)) return 0.0;
+  int e;
+  const double m = frexp(x, &e);
+  int Q = e / q, r = e % q;
+  if (r < 0) { r += q; Q -= 1; }
+  double y = fma(ir_s[q], m, ir_i[q]);
+  for (int it = 0; it < 6; ++it) {
+    double yq = y;
+    for (int j = 1; j < q; ++j) yq = yq * y;
+    y = (y * fma(-m, yq, (double)(q + 1))) * ir_rq[q];
+  }
+  return ldexp(ir_c[q][r] * y, -Q);
+}
+double ref_inv_root(double x, int q) { return inv_root(x, q); }
+
+typedef struct {
+  double t, D[BDF_MAXQ + 3][MAXS], lu[MAXS * MAXS], dinv[MAXS];
+  int piv[MAXS];
+  double yp[MAXS], psi[MAXS], rs[MAXS], d[MAXS], yn[MAXS];
+  double dold, el;
+  int i, conv, fail, nst, live;
+} BdfLane;
+
+/* scipy's change_D for a step-size change by `factor` at order q (D[0..q] <- (R U)^T D), in
+   two stages: E = R(q, factor)^T D, then D = U^T E with U[m][j] = (-1)^m C(j, m) exact
+   (bdf.cuh change_D) */
+static const double bdf_U[6][6] = {{1, 1, 1, 1, 1, 1},    {0, -1, -2, -3, -4, -5}, {0, 0, 1, 3, 6, 10},
+                                   {0, 0, 0, -1, -4, -10}, {0, 0, 0, 0, 1, 5},      {0, 0, 0, 0, 0, -1}};
+static void bdf_change_D(BdfLane* B, int nl, int order, double factor, int S) {
+  double r[6][6]; /* r[m][i] = R[i][m] */
+  for (int m = 1; m <= order; ++m) {
+    double v = 1.0;
+    for (int i = 1; i <= order; ++i) {
+      v = v * (((double)(i - 1) - factor * (double)m) * bdf_inv_i[i]);
+      r[m][i] = v;
+    }
+  }
+  for (int l = 0; l < nl; ++l) {
+    if (!B[l].live) continue;
+    for (int s = 0; s < S; ++s) {
+      double E[6];
+      E[0] = B[l].D[0][s];
+      for (int m = 1; m <= order; ++m) {
+        double e = B[l].D[0][s];
+        for (int i = 1; i <= order; ++i) e = fma(r[m][i], B[l].D[i][s], e);
+        E[m] = e;
+      }
+      for (int j = 0; j <= order; ++j) {
+        double acc = E[0];
+        for (int m = 1; m <= j; ++m) acc = fma(bdf_U[m][j], E[m], acc);
+        B[l].D[j][s] = acc;
+      }
+    }
+  }
+}
+
+/* per-lane max norm of c*v against atol + rtol|y| (argmax by cross-multiplication, one
+   division; non-finite -> 1e30) */
+static double bdf_norm(int S, double c, const double* v, const double* y, double rtol, double atol) {
+  double num = 0.0, den = 1.0, nfe = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const double ae = fabs(c * v[s]);
+    const double sk = fma(rtol, fabs(y[s]), atol);
+    nfe = fma(ae, 0.0, nfe);
+    if (s == 0 || ae * den > num * sk) { num = ae; den = sk; }
+  }
+  double el = num / den;
+  if (!isfinite(el) || isnan(nfe)) el = 1e30;
+  return el;
+}
+
+/* LU factors of I - c J(t, y) */
+static void bdf_factor(const Prob* pb, BdfLane* b, double c, const double* y, double t, const double* p) {
+  const int S = pb->S;
+  double f[MAXS], ft[MAXS];
+  jac_eval(pb, y, t, p, f, b->lu, ft);
+  for (int r = 0; r < S; ++r)
+    for (int cc = 0; cc < S; ++cc) {
+      const double a = c * b->lu[r * S + cc];
+      b->lu[r * S + cc] = (r == cc) ? 1.0 - a : -a;
+    }
+  lu_factor(S, b->lu, b->piv, b->dinv);
+}
+
+static long long g_bdf_stats[3]; /* steps (accepted + rejected), Jacobians, groups */
+void ref_bdf_stats(long long* out, int reset) {
+  for (int j = 0; j < 3; ++j) {
+    out[j] = g_bdf_stats[j];
+    if (reset) g_bdf_stats[j] = 0;
+  }
+}
+
+/* lanes with `part` set start at (t_ev, y0c, grid index i_ev, observation index k_ev) with
+   their accumulators as they are */
+static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
+  static __thread BdfLane B[LANES];
+  const int S = pb->S;
+  const double tend = pb->times[pb->T - 1], t0 = pb->times[0];
+  const double rtol = pb->rtol, atol = pb->atol, ntol = pb->newton_tol;
+  const int tr = traj != NULL;
+  const int budget = BDF_BUDGET * pb->max_steps;
+  long long n_steps = 0, n_jac = 0;
+  double h = INFINITY;
+  for (int l = 0; l < nl; ++l) {
+    BdfLane* b = &B[l];
+    Lane* q = &L[l];
+    b->live = q->part;
+    if (!b->live) continue;
+    const double* pl = p + l * MAXP;
+    b->t = q->t_ev;
+    b->i = q->i_ev;
+    q->kobs = q->k_ev;
+    b->nst = 0;
+    const double* y = q->y0c;
+    double f[MAXS];
+    rhs(pb, y, b->t, pl, f);
+    /* initial step: HINIT for order 1 (max norm), minimum over the lanes */
+    double d0 = 0.0, d1v = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const double sk = atol + rtol * fabs(y[s]);
+      d0 = fmax(d0, fabs(y[s]) / sk);
+      d1v = fmax(d1v, fabs(f[s]) / sk);
+    }
+    const double rest = tend - b->t;
+    double h0 = (d0 <= 1e-5 || d1v <= 1e-5) ? 1e-6 : 0.01 * (d0 / d1v);
+    h0 = fmin(h0, rest);
+    double yt[MAXS], f1[MAXS];
+    for (int s = 0; s < S; ++s) yt[s] = fma(h0, f[s], y[s]);
+    rhs(pb, yt, b->t + h0, pl, f1);
+    double d2 = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const double sk = atol + rtol * fabs(y[s]);
+      d2 = fmax(d2, fabs(f1[s] - f[s]) / sk);
+    }
+    d2 = d2 / h0;
+    const double dm = fmax(d1v, d2);
+    const double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : inv_root(dm / 0.01, 2);
+    double hl = fmin(100.0 * h0, h1);
+    if (!isfinite(hl) || !(hl > 0.0)) hl = rest;
+    h = fmin(h, hl);
+    for (int j = 0; j < BDF_MAXQ + 3; ++j)
+      for (int s = 0; s < S; ++s) b->D[j][s] = 0.0;
+    for (int s = 0; s < S; ++s) { b->D[0][s] = y[s]; b->D[1][s] = f[s]; }
+  }
+  for (int l = 0; l < nl; ++l)
+    if (B[l].live)
+      for (int s = 0; s < S; ++s) B[l].D[1][s] = B[l].D[1][s] * h;
+  const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
+  int order = 1, neq = 0, lu_ok = 0, fresh = 0;
+  for (;;) {
+    int any = 0;
+    for (int l = 0; l < nl; ++l) any |= B[l].live;
+    if (!any) break;
+    ++n_steps;
+    const double c = h * bdf_inv_alpha[order];
+    for (int l = 0; l < nl; ++l) {
+      BdfLane* b = &B[l];
+      if (!b->live) continue;
+      for (int s = 0; s < S; ++s) {
+        double yp = b->D[0][s], ps = 0.0;
+        for (int j = 1; j <= order; ++j) {
+          yp = yp + b->D[j][s];
+          ps = fma(bdf_gamma[j], b->D[j][s], ps);
+        }
+        b->yp[s] = yp;
+        b->psi[s] = ps * bdf_inv_alpha[order];
+        b->rs[s] = 1.0 / fma(rtol, fabs(yp), atol);
+      }
+    }
+    int bad = 0, niter = 0;
+    if (!lu_ok) { /* factors for this step size and order, Jacobian at the current state */
+      for (int l = 0; l < nl; ++l)
+        if (B[l].live) bdf_factor(pb, &B[l], c, B[l].D[0] /* row 0 = the state */, B[l].t, p + l * MAXP);
+      ++n_jac;
+      lu_ok = 1;
+      fresh = 1;
+    }
+    for (;;) {
+      for (int l = 0; l < nl; ++l) {
+        BdfLane* b = &B[l];
+        if (!b->live) continue;
+        memcpy(b->yn, b->yp, sizeof(double) * S);
+        for (int s = 0; s < S; ++s) b->d[s] = 0.0;
+        b->conv = b->fail = 0;
+        b->dold = 0.0;
+      }
+      niter = 0;
+      for (int k = 0; k < BDF_NEWTON_MAXITER; ++k) {
+        int act = 0;
+        for (int l = 0; l < nl; ++l) act |= B[l].live && !B[l].conv && !B[l].fail;
+        if (!act) break;
+        niter = k + 1;
+        for (int l = 0; l < nl; ++l) {
+          BdfLane* b = &B[l];
+          if (!b->live || b->conv || b->fail) continue;
+          double f[MAXS], dy[MAXS], nf = 0.0;
+          rhs(pb, b->yn, b->t + h, p + l * MAXP, f);
+          for (int s = 0; s < S; ++s) {
+            nf = fma(f[s], 0.0, nf);
+            dy[s] = (c * f[s] - b->psi[s]) - b->d[s];
+          }
+          if (isnan(nf)) { b->fail = 1; continue; }
+          lu_solve(S, b->lu, b->piv, b->dinv, dy);
+          double dn = 0.0;
+          for (int s = 0; s < S; ++s) dn = fmax(dn, fabs(dy[s]) * b->rs[s]);
+          double rate = 0.0;
+          if (k > 0) {
+            rate = dn / b->dold;
+            const double pw = (k == 1) ? (rate * rate) * rate : (k == 2) ? rate * rate : rate;
+            if (!(rate < 1.0) || pw / (1.0 - rate) * dn > ntol) { b->fail = 1; continue; }
+          }
+          for (int s = 0; s < S; ++s) {
+            b->yn[s] = b->yn[s] + dy[s];
+            b->d[s] = b->d[s] + dy[s];
+          }
+          if (dn == 0.0 || (k > 0 && rate / (1.0 - rate) * dn < ntol)) b->conv = 1;
+          b->dold = dn;
+        }
+      }
+      bad = 0;
+      for (int l = 0; l < nl; ++l) bad |= B[l].live && !B[l].conv;
+      if (!bad || fresh) break;
+      for (int l = 0; l < nl; ++l)
+        if (B[l].live) bdf_factor(pb, &B[l], c, B[l].yp, B[l].t + h, p + l * MAXP);
+      ++n_jac;
+      fresh = 1;
+    }
+    if (bad) {
+      h = h * 0.5;
+      bdf_change_D(B, nl, order, 0.5, S);
+      neq = 0;
+      lu_ok = 0;
+    } else {
+      const double safety = bdf_safety[niter];
+      double en = 0.0;
+      for (int l = 0; l < nl; ++l) {
+        BdfLane* b = &B[l];
+        if (!b->live) continue;
+        b->el = bdf_norm(S, bdf_ec[order], b->d, b->yn, rtol, atol);
+        en = fmax(en, b->el);
+      }
+      if (en > 1.0) {
+        const double factor = fmax(0.2, safety * inv_root(en, order + 1));
+        h = h * factor;
+        bdf_change_D(B, nl, order, factor, S);
+        neq = 0;
+      } else {
+        /* accepted: differences, grid points, lanes that reach t_end leave */
+        ++neq;
+        fresh = 0;
+        double em = 0.0, ep = 0.0;
+        int voters = 0;
+        for (int l = 0; l < nl; ++l) {
+          BdfLane* b = &B[l];
+          Lane* q = &L[l];
+          if (!b->live) continue;
+          const double tn = b->t + h;
+          for (int s = 0; s < S; ++s) {
+            b->D[order + 2][s] = b->d[s] - b->D[order + 1][s];
+            b->D[order + 1][s] = b->d[s];
+          }
+          for (int j = order; j >= 0; --j)
+            for (int s = 0; s < S; ++s) b->D[j][s] = b->D[j][s] + b->D[j + 1][s];
+          ++b->nst;
+          double yo[MAXS];
+          while (b->i < pb->T && pb->times[b->i] <= tn) {
+            const double ti = pb->times[b->i];
+            double prod = 1.0;
+            for (int s = 0; s < S; ++s) yo[s] = b->D[0][s];
+            for (int j = 1; j <= order; ++j) {
+              const double x = (ti - (tn - (double)(j - 1) * h)) / ((double)j * h);
+              prod = prod * x;
+              for (int s = 0; s < S; ++s) yo[s] = fma(b->D[j][s], prod, yo[s]);
+            }
+            if (needs_emit(pb, tr, b->i, q->kobs)) emit(pb, b->i, yo, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
+            ++b->i;
+            b->nst = 0;
+          }
+          b->t = tn;
+          if (b->i >= pb->T) { /* done: the final state is the last grid point's */
+            memcpy(q->y, yo, sizeof(double) * S);
+            b->live = 0;
+            continue;
+          }
+          if (neq >= order + 1) {
+            ++voters;
+            if (order > 1) em = fmax(em, bdf_norm(S, bdf_ec[order - 1], b->D[order], b->yn, rtol, atol));
+            if (order < BDF_MAXQ) ep = fmax(ep, bdf_norm(S, bdf_ec[order + 1], b->D[order + 2], b->yn, rtol, atol));
+          }
+        }
+        if (neq >= order + 1 && voters) {
+          const double fm = (order > 1) ? inv_root(em, order) : 0.0;
+          const double fe = inv_root(en, order + 1);
+          const double fp = (order < BDF_MAXQ) ? inv_root(ep, order + 2) : 0.0;
+          int dq = 0;
+          double fmx = fm;
+          if (fe > fmx) { fmx = fe; dq = 1; }
+          if (fp > fmx) { fmx = fp; dq = 2; }
+          order += dq - 1;
+          const double factor = fmin(10.0, safety * fmx);
+          h = h * factor;
+          bdf_change_D(B, nl, order, factor, S);
+          neq = 0;
+          lu_ok = 0;
+        }
+      }
+    }
+    /* budget: a lane that needs more than `budget` steps inside one output interval, or a
+       step below hmin, is abandoned (MAXSTEP, NaN for the rest of its grid) */
+    for (int l = 0; l < nl; ++l) {
+      BdfLane* b = &B[l];
+      Lane* q = &L[l];
+      if (!b->live || (b->nst < budget && !(h < hmin))) continue;
+      b->live = 0;
+      q->a.status |= ST_MAXSTEP;
+      double yo[MAXS];
+      for (int s = 0; s < S; ++s) yo[s] = NAN;
+      for (; b->i < pb->T; ++b->i)
+        if (needs_emit(pb, tr, b->i, q->kobs)) emit(pb, b->i, yo, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
+      memcpy(q->y, yo, sizeof(double) * S);
+    }
+  }
+  for (int l = 0; l < nl; ++l)
+    if (L[l].part) check_finite(S, L[l].y, &L[l].a);
+#pragma omp atomic
+  g_bdf_stats[0] += n_steps;
+#pragma omp atomic
+  g_bdf_stats[1] += n_jac;
+#pragma omp atomic
+  g_bdf_stats[2] += 1;
+}
+
+/* 'auto': DOPRI5 with the stiffness test; S <= 8: the lanes it evicts continue from the
+   eviction point with BDF; wider models: evicted walkers again from t0 by RODAS */
 static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
   const int S = pb->S;
+  if (S <= 8) {
+    dopri5_group(pb, L, nl, p, traj, W, 1);
+    int any = 0;
+    for (int l = 0; l < nl; ++l) {
+      L[l].part = L[l].handed && L[l].active;
+      any |= L[l].part;
+      if (L[l].part) L[l].a.status |= ST_STIFF;
+    }
+    if (any) bdf_group(pb, L, nl, p, traj, W);
+    return;
+  }
   for (int l = 0; l < nl; ++l) memcpy(L[l].y0c, L[l].y, sizeof(double) * S);
   dopri5_group(pb, L, nl, p, traj, W, 1);
   int any = 0;
@@ -817,7 +1249,8 @@ static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double*
 static Prob make_prob(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                       const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                       int substeps, double rtol, double atol, int max_steps) {
-  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol, 0, 0};
+  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol, 0, 0, 0};
+  pb.newton_tol = bdf_newton_tol(rtol);
   return pb;
 }
 
@@ -860,6 +1293,18 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
     dopri5_group(pb, L, G, p, traj, W, 0);
   } else if (pb->method == METHOD_AUTO) {
     auto_group(pb, L, LANES, p, traj, W);
+  } else if (pb->method == METHOD_BDF) {
+    for (int l = 0; l < LANES; ++l) {
+      Lane* q = &L[l];
+      q->part = q->active;
+      q->kobs = 0;
+      if (q->active) emit(pb, 0, q->y, traj, W, q->w, &q->kobs, &q->a);
+      memcpy(q->y0c, q->y, sizeof(double) * pb->S);
+      q->t_ev = pb->times[0];
+      q->i_ev = 1;
+      q->k_ev = q->kobs;
+    }
+    bdf_group(pb, L, LANES, p, traj, W);
   } else {
     for (int l = 0; l < LANES; ++l) L[l].part = L[l].active;
     if (pb->wave_redo) {

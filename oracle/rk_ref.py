@@ -42,6 +42,12 @@ def lib():
         L.ref_philox_draws.argtypes = [u64, u64, i32, i32, vp, vp]
         L.ref_dopri5_stats.restype = None
         L.ref_dopri5_stats.argtypes = [vp, i32]
+        L.ref_rosenbrock_stats.restype = None
+        L.ref_rosenbrock_stats.argtypes = [vp, i32]
+        L.ref_bdf_stats.restype = None
+        L.ref_bdf_stats.argtypes = [vp, i32]
+        L.ref_inv_root.restype = d
+        L.ref_inv_root.argtypes = [d, i32]
         _lib = L
     return _lib
 
@@ -50,7 +56,7 @@ def _p(a):
     return None if a is None else a.ctypes.data
 
 
-METHODS = {"rk4": 0, "dopri5": 1, "auto": 2, "rosenbrock": 3}
+METHODS = {"rk4": 0, "dopri5": 1, "auto": 2, "rosenbrock": 3, "bdf": 4}
 
 
 class Problem:
@@ -145,6 +151,25 @@ def dopri5_stats(reset: bool = True) -> dict:
     out = np.zeros(3, np.int64)
     lib().ref_dopri5_stats(out.ctypes.data, int(reset))
     return {"accepted": int(out[0]), "rejected": int(out[1]), "groups": int(out[2])}
+
+
+def rosenbrock_stats(reset: bool = True) -> dict:
+    """Rosenbrock lockstep steps (accepted + rejected) and groups since the last reset."""
+    out = np.zeros(2, np.int64)
+    lib().ref_rosenbrock_stats(out.ctypes.data, int(reset))
+    return {"steps": int(out[0]), "groups": int(out[1])}
+
+
+def bdf_stats(reset: bool = True) -> dict:
+    """BDF lockstep steps (accepted + rejected), Jacobian evaluations and groups since the last reset."""
+    out = np.zeros(3, np.int64)
+    lib().ref_bdf_stats(out.ctypes.data, int(reset))
+    return {"steps": int(out[0]), "jacobians": int(out[1]), "groups": int(out[2])}
+
+
+def inv_root(x: float, q: int) -> float:
+    """x^(-1/q) as the BDF step controller computes it (oracle/rk_ref.c inv_root)."""
+    return lib().ref_inv_root(float(x), int(q))
 
 
 def inv_fifth_root(x: float) -> float:

@@ -1,5 +1,6 @@
-"""GPU parity of the stiff methods (OE_METHOD_AUTO: DOPRI5 + stiffness test + Rosenbrock
-restart; OE_METHOD_ROSENBROCK) through the C-ABI:
+"""GPU parity of the stiff methods (OE_METHOD_AUTO: DOPRI5 + stiffness test, evicted lanes
+continue with BDF (S <= 8) or restart with RODAS (wider); OE_METHOD_BDF; OE_METHOD_ROSENBROCK)
+through the C-ABI:
 
 * same algorithm (oracle/rk_ref.c): trajectories and status bitwise, chi rtol 1e-12
   (ocml vs libm log), on waves that mix the demo draws with stiff ones;
@@ -54,7 +55,7 @@ def _radau(ode, y0, times, th):
     return sol.y.T
 
 
-@pytest.mark.parametrize("method", ["auto", "rosenbrock"])
+@pytest.mark.parametrize("method", ["auto", "rosenbrock", "bdf"])
 @pytest.mark.parametrize("W,stiff", [(1, [0]), (70, [3, 64, 69]), (200, [0, 1, 2, 130, 199])])
 def test_stiff_methods_bitwise_vs_c_restatement(method, W, stiff):
     m = product_model("two_i", method=method)
@@ -71,8 +72,9 @@ def test_stiff_methods_bitwise_vs_c_restatement(method, W, stiff):
 
 
 def test_auto_moderately_stiff_walkers_bitwise_vs_c_restatement():
-    """The weighted, cost-gated stiffness test (tau = 1e3 .. 3e4 lanes in demo waves):
-    the same walkers flagged as the C restatement, trajectories bitwise."""
+    """The weighted, cost-gated stiffness test (tau = 1e3 .. 3e4 lanes in demo waves): the
+    same walkers flagged as the C restatement — every one of them, the hand-over to BDF
+    being cheap — handed over at their own times, trajectories bitwise."""
     m = product_model("two_i", method="auto")
     W = 130
     theta = walker_thetas("two_i", W).T.copy()
@@ -84,12 +86,13 @@ def test_auto_moderately_stiff_walkers_bitwise_vs_c_restatement():
     assert np.array_equal(out["traj"], ref["traj"], equal_nan=True)
     assert np.array_equal(out["status"], ref["status"])
     np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
-    assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == [64, 100, 129]
+    assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == [5, 40, 64, 100, 129]
 
 
+@pytest.mark.parametrize("method", ["rosenbrock", "bdf"])
 @pytest.mark.parametrize("name", ["zero_i", "one_i"])
-def test_rosenbrock_other_models_bitwise(name):
-    m = product_model(name, method="rosenbrock")
+def test_rosenbrock_other_models_bitwise(name, method):
+    m = product_model(name, method=method)
     theta = walker_thetas(name, 66).T.copy()
     y0, out = _run(m, theta)
     ref = rk_ref.integrate(m.fit_problem(), y0, theta)
@@ -97,7 +100,7 @@ def test_rosenbrock_other_models_bitwise(name):
     assert np.array_equal(out["status"], ref["status"])
 
 
-@pytest.mark.parametrize("method", ["auto", "rosenbrock"])
+@pytest.mark.parametrize("method", ["auto", "rosenbrock", "bdf"])
 def test_stiff_walkers_vs_tight_implicit_solution(method):
     m = product_model("two_i", method=method)
     W = 64
@@ -132,13 +135,13 @@ def test_auto_chi_only_mode_equals_trajectory_mode():
         assert np.array_equal(a[k], b[k]), k
 
 
-@pytest.mark.parametrize("method", ["auto", "rosenbrock"])
+@pytest.mark.parametrize("method", ["auto", "rosenbrock", "bdf"])
 def test_mh_stiff_methods_vs_c_restatement(method):
     """Philox MH chains where some proposals are stiff: the device chain equals the C
     restatement's (rtol 1e-8 as for DOPRI5 MH: ocml vs libm exp/log in the proposal)."""
-    W = 128 if method == "auto" else 8  # (the C restatement of RODAS for every chain is slow)
+    W = 8 if method == "rosenbrock" else 128  # (the C restatement of RODAS for every chain is slow)
     m = product_model("two_i", method=method)
-    theta = _mixed_thetas("two_i", W, [1, 64, 65, 127] if method == "auto" else [1])
+    theta = _mixed_thetas("two_i", W, [1] if method == "rosenbrock" else [1, 64, 65, 127])
     y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
     walk = np.ones(5, np.uint8)
     dev = m.engine().mh_run(theta, y0, nits=12, burnin=4, walk_mask=walk, rng="philox", seed=11)
@@ -146,12 +149,13 @@ def test_mh_stiff_methods_vs_c_restatement(method):
     np.testing.assert_allclose(dev["samples"].cpu().numpy(), ref["samples"], rtol=1e-8)
 
 
-def test_rtc_templated_body_gets_stiff_methods_bitwise():
+@pytest.mark.parametrize("method", ["auto", "bdf"])
+def test_rtc_templated_body_gets_stiff_methods_bitwise(method):
     """A user C body written over the scalar type R compiles for dual numbers: the RTC
     module has the stiff methods and reproduces the built-in kernels bitwise."""
     theta = _mixed_thetas("two_i", 96, [2, 50])
-    a = product_model("two_i", method="auto")
-    b = product_model("two_i", method="auto", device_rhs=TWO_I_TEMPLATED_BODY)
+    a = product_model("two_i", method=method)
+    b = product_model("two_i", method=method, device_rhs=TWO_I_TEMPLATED_BODY)
     _, ra = _run(a, theta)
     _, rb = _run(b, theta)
     for k in ("traj", "chi", "ssres", "status"):
@@ -252,8 +256,8 @@ def test_default_method_is_auto_with_dopri5_fallback():
         e.engine()
 
 
-@pytest.mark.parametrize("n", [6, 10, 20])
-@pytest.mark.parametrize("method", ["auto", "rosenbrock"])
+@pytest.mark.parametrize("n,method", [(6, "auto"), (10, "auto"), (20, "auto"), (6, "rosenbrock"), (10, "rosenbrock"),
+                                      (20, "rosenbrock"), (6, "bdf"), (8, "bdf")])
 def test_wide_chain_stiff_methods_bitwise_vs_c_restatement(n, method):
     """S = 6: the register path (wave-shared step); S = 10, 20: one wave per stiff
     walker (k_stiff_wave, the walker's own step; the C restatement redoes wide walkers one
@@ -261,7 +265,7 @@ def test_wide_chain_stiff_methods_bitwise_vs_c_restatement(n, method):
     two-wave ensemble with stiff lanes in both waves."""
     from helpers import chain_problem
     m = chain_problem(n, method=method)
-    W, stiff = (70, [3, 64, 69]) if method == "auto" else (6, [1, 4])
+    W, stiff = (70, [3, 64, 69]) if method in ("auto", "bdf") else (6, [1, 4])
     theta = _mixed_thetas("two_i", W, stiff)
     y0, out = _run(m, theta)
     ref = rk_ref.integrate(m.fit_problem(), y0, theta)
@@ -285,3 +289,35 @@ def test_wide_chain_mh_auto_vs_c_restatement():
     dev = m.engine().mh_run(theta, y0, nits=6, burnin=2, walk_mask=walk, rng="philox", seed=5)
     ref = rk_ref.mh_run(m.fit_problem(), theta, y0, 6, 2, walk, rng="philox", seed=5)
     np.testing.assert_allclose(dev["samples"].cpu().numpy(), ref["samples"], rtol=1e-8)
+
+
+def test_auto_demo_fit_region_bitwise_and_vs_tight_solution():
+    """The draws that made the notebook's fit slow (phi ~ 1e-4: the host is infected within
+    ~1e-3 time units and its relative decay then sets DOPRI5 to crawl at h|lambda| ~ 3.3
+    for the rest of the span; tau ~ 1e2 .. 2e2, beta up to 4e2) in waves of demo draws:
+    bitwise the C restatement (lanes handed to BDF at their own times), within 1e-6 of
+    tight Radau."""
+    m = product_model("two_i", method="auto")
+    W = 130
+    theta = walker_thetas("two_i", W, seed=9).T.copy()
+    theta[1, [2, 70, 129]] = [1.06e-4, 8.8e-5, 5.0e-6]
+    theta[4, [10, 71]] = [99.0, 218.0]
+    theta[2, 40] = 415.0
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"], equal_nan=True)
+    assert np.array_equal(out["status"], ref["status"])
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
+    assert {2, 70} <= set(np.nonzero(out["status"] & 8)[0].tolist())
+    for w in (2, 10, 40, 70, 71, 129, 0):
+        r = _radau(CONFIGS["two_i"]["ode"], y0[:, w], m.times, theta[:, w])
+        np.testing.assert_allclose(out["traj"][:, :, w], r, rtol=1e-6, atol=1e-6, err_msg=str(w))
+
+
+def test_bdf_refused_above_register_path():
+    """'bdf' is the register path's (n_states <= 8): a wider model is refused, not replaced."""
+    from helpers import chain_problem
+    from odelib_amd import _native as N
+    with pytest.raises(N.NativeUnsupported):
+        chain_problem(10, method="bdf").engine()
+    chain_problem(6, method="bdf").engine()

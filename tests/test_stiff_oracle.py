@@ -134,7 +134,7 @@ def _radau(fp, y0, th):
     return sol.y.T
 
 
-@pytest.mark.parametrize("method", ["rosenbrock", "auto"])
+@pytest.mark.parametrize("method", ["rosenbrock", "auto", "bdf"])
 def test_stiff_methods_match_tight_implicit_solution(method):
     """odeint's default tolerances; every walker — stiff or not — within
     1e-6·|y| + 1e-6 of the tight implicit solution, the bar the explicit methods meet on
@@ -155,14 +155,27 @@ def test_auto_switch_is_scale_invariant_and_cost_aware():
     """The stiffness test weighs each component by the error control's scale, so a stiff
     mode in a small compartment is seen next to the 1e7-sized host/virus states
     (unweighted, tau = 1e4 and 3e4 were never flagged and DOPRI5 crawled 10-30x the normal
-    work); a flagged walker is handed over only while DOPRI5 would need more than ~4000
-    more steps (tau = 1e3, 3e3 stay with DOPRI5, which is cheaper there).  Every walker
-    within the 1e-6 bar of tight Radau."""
-    taus = [1e3, 3e3, 1e4, 3e4]
+    work).  The hand-over to BDF continues from the eviction point, so it is taken whenever
+    DOPRI5 would need more than 300 more steps at h|lambda| > 2.5, or more than 1500 at
+    h|lambda| > 0.5: tau = 1e2 stays with DOPRI5, tau = 1e3 (accuracy-limited at
+    h|lambda| ~ 0.9: 2 359 DOPRI5 steps) and up are handed over.  Every walker within the
+    1e-6 bar of tight Radau, and the hand-over costs far fewer steps than DOPRI5 alone."""
+    taus = [1e2, 1e3, 3e3, 1e4, 3e4]
     fp, theta, y0 = _problem("auto", ["nonstiff"] * len(taus))
     theta[4, :] = taus
     out = rk_ref.integrate(fp, y0, theta)
-    assert [bool(s & 8) for s in out["status"]] == [False, False, True, True]
+    assert [bool(s & 8) for s in out["status"]] == [False, True, True, True, True]
+    for w, tau in enumerate(taus[1:], 1):
+        th = theta[:, w:w + 1].copy()
+        steps = {}
+        for meth in ("dopri5", "auto"):
+            fp.method = meth
+            rk_ref.dopri5_stats(True), rk_ref.bdf_stats(True)
+            rk_ref.integrate(fp, y0[:, w:w + 1].copy(), th, trajectory=False)
+            steps[meth] = sum(rk_ref.dopri5_stats(True)[k] for k in ("accepted", "rejected")) + \
+                rk_ref.bdf_stats(True)["steps"]
+        assert steps["auto"] < 0.3 * steps["dopri5"], (tau, steps)
+    fp.method = "auto"
     assert not (out["status"] & 4).any()
     for w in range(len(taus)):
         ref = _radau(fp, y0[:, w], theta[:, w])
@@ -210,7 +223,7 @@ def test_auto_chi_at_least_as_accurate_as_reference_odeint():
 
 def test_stiff_walker_in_a_wave_of_nonstiff_ones():
     """One stiff walker among 63 demo draws: it is evicted from the shared DOPRI5 step and
-    redone by RODAS; every walker stays within tolerance of the tight solution, and the
+    continues with BDF; every walker stays within tolerance of the tight solution, and the
     wave's step count stays that of the non-stiff draws (the stiff lane does not pin it)."""
     m = product_model("two_i")
     fp = m.fit_problem()
@@ -249,3 +262,59 @@ def test_wide_chain_stiff_walkers_match_tight_implicit_solution(n):
     st = out["status"]
     assert not (st & 4).any()
     assert [bool(s & 8) for s in st] == [k != "nonstiff" for k in sets]
+
+
+def test_inv_root_accuracy():
+    """x^(-1/q), q = 1..6, of the BDF step controller (frexp/ldexp + Newton, bit-identical on
+    the device): within 1e-15 relative of the long-double value; 0 -> inf, inf -> 0."""
+    xs = np.concatenate([[5e-324, 1e-310, 2.2250738585072014e-308, 1e-30, 1.0, 1e30, 1.7e308],
+                         np.logspace(-300, 300, 2001), np.random.RandomState(3).uniform(0.5, 40.0, 1000)])
+    for q in range(1, 7):
+        for x in xs:
+            got = rk_ref.inv_root(x, q)
+            want = float(np.exp(-np.log(np.longdouble(x)) / q))
+            if np.isinf(want):  # 1/x beyond the double range: overflows alike
+                assert got == want, (q, x, got)
+                continue
+            assert abs(got / want - 1.0) < 2e-15, (q, x, got, want)
+    assert rk_ref.inv_root(0.0, 3) == np.inf and rk_ref.inv_root(np.inf, 2) == 0.0
+
+
+def test_bdf_step_counts_are_lsoda_like_where_explicit_and_rosenbrock_methods_are_not():
+    """The reason 'auto' hands stiff lanes to BDF and not to RODAS: on a
+    stiff component sitting on its quasi-steady state (two_i, tau = 1e4) the one-step
+    Rosenbrock method suffers order reduction (~3 700 steps at odeint's tolerances) and DOPRI5
+    crawls at its stability limit (~12 000), while BDF takes LSODA-like step counts (~600;
+    scipy's BDF: 546, LSODA: 734).  Measured on the C restatement."""
+    fp, theta, y0 = _problem("bdf", ["nonstiff"])
+    theta[4, 0] = 1e4
+    steps = {}
+    for meth in ("dopri5", "rosenbrock", "bdf"):
+        fp.method = meth
+        rk_ref.dopri5_stats(True), rk_ref.rosenbrock_stats(True), rk_ref.bdf_stats(True)
+        rk_ref.integrate(fp, y0, theta, trajectory=False)
+        d, r, b = rk_ref.dopri5_stats(True), rk_ref.rosenbrock_stats(True), rk_ref.bdf_stats(True)
+        steps[meth] = d["accepted"] + d["rejected"] + r["steps"] + b["steps"]
+    assert steps["bdf"] < 700 and steps["rosenbrock"] > 3000 and steps["dopri5"] > 10000, steps
+
+
+def test_bdf_handover_in_a_lockstep_group_matches_tight_solution():
+    """'auto' lanes handed over at different times (tau = 1e3 .. 1e5, the demo's phi ~ 1e-4
+    region) continue with their own time and a shared BDF step: all within the 1e-6 bar
+    of tight Radau, the others untouched by the hand-over (DOPRI5's own trajectory)."""
+    m = product_model("two_i")
+    fp = m.fit_problem()
+    W = 64
+    theta = walker_thetas("two_i", W).T.copy()
+    lanes = {3: (4, 1e3), 17: (4, 1e5), 30: (1, 1.0e-4), 31: (4, 3e4), 50: (1, 6e-6)}
+    for w, (j, v) in lanes.items():
+        theta[j, w] = v
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    fp.method = "auto"
+    out = rk_ref.integrate(fp, y0, theta)
+    flagged = [w for w in range(W) if out["status"][w] & 8]
+    assert set(flagged) >= {3, 17, 30, 31}, flagged
+    assert not (out["status"] & 4).any()
+    for w in list(lanes) + [0, 63]:
+        ref = _radau(fp, y0[:, w], theta[:, w])
+        np.testing.assert_allclose(out["traj"][:, :, w], ref, rtol=1e-6, atol=1e-6, err_msg=str(w))
