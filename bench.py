@@ -40,6 +40,8 @@ rank 0 at N=1 only.
 from __future__ import annotations
 
 import argparse
+import contextlib
+import io
 import json
 import os
 import subprocess
@@ -87,6 +89,9 @@ def parse():
                     help="wide chain models' DOPRI5: one lane per walker instead of the split kernel")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg (1 048 576 walkers over the ranks)")
     ap.add_argument("--c4-steps", type=int, default=10, help="C4 leg: timed trajectory integrates")
+    ap.add_argument("--pool", default="cabi", choices=["cabi", "torch"],
+                    help="C4 posterior pooling: the C-ABI's RCCL communicator (oe_allgather_samples, what "
+                         "ODElib binds) or torch.distributed's all_gather_into_tensor")
     return ap.parse_args()
 
 
@@ -351,6 +356,89 @@ def cpu_mcmc_baseline(m, chains=32, nits=101, full_nits=1001):
                       f"lognorm priors' pdf/rvs), Pool({len(jobs)}); scaled to {full_nits - 1} iterations"}
 
 
+DEMO_CHAINS, DEMO_NITS = 32, 1001  # the notebook's fit: MCMC(chain_inits=32), 1000 iterations
+
+
+def demo_model():
+    """The notebook's fit model (Demo_InfectionStates.ipynb: two_i, lognorm priors, demodata,
+    H = S + I1 + I2), as tools/demo_fit.py builds it."""
+    import pandas as pd
+    import scipy.stats
+    from odelib_amd import ModelFramework, parameter
+    from odelib_amd.models import BUILTIN
+    df = pd.read_csv(os.path.join(ROOT, "tests", "golden", "demodata.csv")).replace({"virus": "V", "host": "H"})
+    pn = ["mu", "phi", "beta", "lam", "tau"]
+    pars = {p: parameter(stats_gen=scipy.stats.lognorm, hyperparameters=dict(NOTEBOOK_PRIORS[p]), init_value=v)
+            for p, v in zip(pn, THETA_STAR)}
+    return ModelFramework(ODE=BUILTIN["two_i"][3], parameter_names=pn, state_names=["S", "I1", "I2", "V"],
+                          dataframe=df, state_summations={"H": ["S", "I1", "I2"]}, S=5236900, **pars)
+
+
+def demo_fit_starts(m, n=DEMO_CHAINS):
+    """The notebook fit's chain starts, on the host (no GPU): ``MCMC(chain_inits=n,
+    fitsurvey_samples=10000, sd_fitdistance=6.0)``'s survey (Framework.py:993-1012) — LHS
+    draws through the priors, chi of each by the C restatement of the device integrator
+    ('auto'; oracle/rk_ref.c), the samples whose chi beats the data shifted by 6 log sigmas,
+    drawn with replacement by pandas — numpy's global RNG seeded as tools/demo_fit.py does.
+    The CPU baseline and the device run then start their chains from the SAME parameters."""
+    import numpy as np
+    from oracle import rk_ref
+
+    def survey(samples=1000, cpu_cores=1):
+        ps = m._lhs_samples(samples)[m.get_pnames()]
+        th = np.ascontiguousarray(ps.to_numpy(dtype=float).T)
+        y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], th.shape[1], axis=1)
+        out = ps.reset_index(drop=True)
+        out["chi"] = rk_ref.integrate(m.fit_problem(), y0, th, trajectory=False)["chi"]
+        return out
+    np.random.seed(20261017 + n)
+    saved, m.fit_survey = m.fit_survey, survey
+    try:
+        starts = m._survey_chain_starts(n, 10000, 6.0, 8)
+    finally:
+        m.fit_survey = saved
+    return [starts.iloc[i][m.get_pnames()].to_dict() for i in range(n)]
+
+
+_DEMO_ORACLE = None
+
+
+def _cpu_demo_worker(args):
+    chains, nits = args
+    import numpy as np
+    from oracle import cpu_ref
+    t0 = time.perf_counter()
+    for c, start in chains:
+        for p, v in start.items():
+            _DEMO_ORACLE.parameters[p].val = np.float64(v)
+        _DEMO_ORACLE.random_seed = c
+        cpu_ref.metropolis_hastings(_DEMO_ORACLE, nits=nits)
+    return len(chains) * (nits - 1), time.perf_counter() - t0
+
+
+def cpu_demo_fit_baseline(m, starts, nits=101, full_nits=DEMO_NITS):
+    """The reference's MCMC loop (Samplers.py:53-174 via oracle/cpu_ref.py: scipy odeint =
+    LSODA, the lognorm priors' pdf/rvs, chain i seeded i as Framework.py:1015) from the notebook
+    fit's chain starts (demo_fit_starts), one chain per pool task (Framework.py:779) on the
+    host cores; a bounded sample of the first ``nits`` iterations, scaled to ``full_nits``."""
+    import multiprocessing as mp
+    global _DEMO_ORACLE
+    _DEMO_ORACLE = _oracle_mh_model(m)
+    cores, _ = host_cores()
+    idx = list(enumerate(starts))
+    jobs = [([cs for cs in idx if cs[0] % cores == k], nits) for k in range(min(cores, len(starts)))]
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(len(jobs)) as pool:
+        res = pool.map(_cpu_demo_worker, jobs)
+    wall = time.perf_counter() - t0
+    return {"wall_s_sample": wall, "chain_iterations_sample": sum(r[0] for r in res), "cores": len(jobs),
+            "wall_s_scaled_to_full_run": wall * (full_nits - 1) / (nits - 1),
+            "ms_per_iteration_scaled": wall / (nits - 1) * 1e3,
+            "sample": f"the notebook fit's {len(starts)} chains (same LHS starts as the device leg) x {nits - 1} "
+                      f"iterations of the reference MH loop (scipy odeint, lognorm priors' pdf/rvs, seed = chain), "
+                      f"Pool({len(jobs)}); scaled to {full_nits - 1} iterations"}
+
+
 def cpu_rk4_c(fp, y0, W, cores):
     """The same fixed-step RK4 + fused likelihood in C (oracle/rk_ref.c, OpenMP over
     64-walker groups, interval-major so rows are written as runs of walkers) on the
@@ -372,6 +460,22 @@ def cpu_rk4_c(fp, y0, W, cores):
     return {"value": W * (T - 1) / best, "unit": "walker-timesteps/s", "cores": cores, "kind": "port",
             "sample": f"{W} walkers x {T - 1} intervals, RK4 + trajectory store + chi in C "
                       f"(oracle/rk_ref.c, gcc -O2, OpenMP {cores} threads), best of 2: {best:.2f} s"}
+
+
+def tolerance_of(model: str, method: str, substeps: int, rtol: float, atol: float) -> str:
+    """The accuracy the bench's configuration is pinned to (the tests that pin it):
+    RK4 is fixed-step, so its bar is what tests/test_gpu_parity.py checks against tight
+    odeint for that model and substep count; the adaptive methods run at the problem's
+    rtol/atol (odeint's defaults) and are checked within 1e-6 of tight odeint / Radau."""
+    if method == "rk4":
+        if model == "two_i" and substeps >= 1:
+            return "vs tight odeint: rtol 1e-6, atol 1e-6 (test-pinned, rk4_substeps=%d)" % substeps
+        if model == "chain20":
+            return ("vs tight odeint: rtol 1e-6, atol 1e-4 (test-pinned)" if substeps < 3
+                    else "vs tight odeint: rtol 1e-6, atol 1e-6 (test-pinned)")
+        return "fixed step (rk4_substeps=%d); not pinned for this model" % substeps
+    return "rtol=%g, atol=%g (%s; within 1e-6 of tight odeint, test-pinned)" % (
+        rtol, atol, "odeint defaults" if rtol == atol == 1.49012e-8 else "user tolerances")
 
 
 def write_ceiling(buf, stream, launches=20, warm_ms=60.0):
@@ -560,10 +664,27 @@ def c4_leg(args, R, T, P):
     res["mh"] = {"iterations": C4_NITS, "burnin": burn, "wall_s": t_mh,
                  "walker_timesteps_per_s": C4_WALKERS * (T - 1) * C4_NITS / t_mh,
                  "kernel_ms_rank0": eng.last_kernel_ms()}
-    # (3) the ONE posterior all-gather (Framework.py:1037 pd.concat analogue)
+    # (3) the ONE posterior all-gather (Framework.py:1037 pd.concat analogue).  --pool cabi:
+    # the C-ABI's own RCCL communicator (oe_comm + oe_allgather_samples: pad, ncclAllGather,
+    # rank-major -> walker-minor re-layout), the path INTEGRATION.md gives ODElib; it needs
+    # one GPU per rank (RCCL), so a gloo rehearsal with ranks sharing a GPU pools with torch.
+    # At N = 1 the C-ABI path still runs (a 1-rank communicator) so its fields are reported.
     blk = r["samples"]
     res["posterior_block_bytes_per_rank"] = blk.numel() * 8
-    if R.world > 1:
+    pool = args.pool if (R.world == 1 or R.backend == "nccl") else "torch"
+    if pool == "cabi":
+        from odelib_amd.distributed import native_allgather_walkers, native_comm
+        comm = native_comm(R.dev.index, None)
+        src = blk.contiguous()
+        native_allgather_walkers(src[:1], C4_WALKERS if R.world > 1 else cnt, comm)  # untimed: channel set-up
+        R.fence()
+        t0 = time.perf_counter()
+        pooled = native_allgather_walkers(src, C4_WALKERS if R.world > 1 else cnt, comm)
+        R.fence()
+        t_ag = R.max(time.perf_counter() - t0)
+        n_ranks = comm.n_ranks
+        comm.close()
+    elif R.world > 1:
         src = blk.contiguous() if R.backend == "nccl" else blk.cpu()
         allgather_walkers(src[:1], C4_WALKERS)  # untimed: communicator / channel set-up
         R.fence()
@@ -571,14 +692,20 @@ def c4_leg(args, R, T, P):
         pooled = allgather_walkers(src, C4_WALKERS)
         R.fence()
         t_ag = R.max(time.perf_counter() - t0)
-        assert pooled.shape[-1] == C4_WALKERS
+        n_ranks = R.world
+    else:
+        pooled = None
+    if pooled is not None:
+        assert pooled.shape[-1] == (C4_WALKERS if R.world > 1 else cnt)
         gathered = pooled.numel() * 8
-        res["allgather"] = {"backend": R.backend, "bytes_gathered": gathered, "s": t_ag,
-                            "algbw_GBps": gathered / t_ag / 1e9,
+        res["allgather"] = {"pool": pool, "backend": "rccl (oe_comm)" if pool == "cabi" else R.backend,
+                            "comm_n_ranks": n_ranks, "world_size": R.world, "bytes_gathered": gathered,
+                            "s": t_ag, "algbw_GBps": gathered / t_ag / 1e9,
                             "busbw_GBps": gathered * (R.world - 1) / R.world / t_ag / 1e9}
         del pooled
     else:
-        res["allgather"] = None  # one GPU: nothing to pool
+        res["allgather"] = {"pool": "torch", "comm_n_ranks": 1, "world_size": 1,
+                            "note": "one GPU, torch pooling: nothing to gather"}
     del r, blk
     torch.cuda.empty_cache()
     return res
@@ -685,6 +812,41 @@ def small_mcmc(R, T, P, nits=1001):
     return out
 
 
+def demo_fit_leg(demo, cpu):
+    """The notebook's fit on the device through the drop-in API: ``MCMC`` from the chain
+    starts the CPU baseline used (demo_fit_starts), 32 chains x 1000 iterations, the default
+    method ('auto'), the reference's numpy draws (rng='replay', chain i seeded i), with one
+    iteration per step and with speculative rounds; beside it the synthetic 32-chain 'auto'
+    MH (small_mcmc) for the per-iteration ratio."""
+    import numpy as np
+    import torch
+    m, starts = demo["model"], demo["starts"]
+    row = {"workload": f"the notebook fit: MCMC from {len(starts)} LHS chain starts (fitsurvey_samples=10000, "
+                       f"sd_fitdistance=6), {DEMO_NITS - 1} iterations, method {m.method}, rng replay"}
+    m.MCMC(chain_inits=starts[:2], iterations_per_chain=5, print_report=False, print_iterations=False)  # warm
+    posts = {}
+    for spec in (0, "auto"):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            posts[spec] = m.MCMC(chain_inits=starts, iterations_per_chain=DEMO_NITS - 1, print_report=False,
+                                 print_iterations=False, speculate=spec)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        row[f"wall_s_speculate_{spec}"] = wall
+        row[f"ms_per_iteration_speculate_{spec}"] = wall / (DEMO_NITS - 1) * 1e3
+        row[f"depth_{spec}"] = m.engine().last_mh_depth()
+    pn = m.get_pnames()
+    row["same_parameters"] = bool(np.array_equal(posts[0][pn].to_numpy(), posts["auto"][pn].to_numpy()))
+    row["posterior_q99_max"] = {p: [float(posts[0][p].quantile(0.99)), float(posts[0][p].max())]
+                                for p in ("phi", "beta", "lam", "tau")}
+    if cpu and "mcmc_demo_fit_32chains" in cpu:
+        c = cpu["mcmc_demo_fit_32chains"]
+        row["cpu_reference_ms_per_iteration"] = c["ms_per_iteration_scaled"]
+        row["speedup_vs_cpu_speculate_auto"] = c["ms_per_iteration_scaled"] / row["ms_per_iteration_speculate_auto"]
+    return row
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
@@ -711,6 +873,12 @@ def main():
             cpu["rk4_c_openmp"] = cpu_rk4_c(fp_host, y0h, args.walkers, cpu["cores"])
         if args.model == "two_i" and not args.no_extra_configs:
             cpu["mcmc_32chains"] = cpu_mcmc_baseline(m)
+    demo = None
+    if args.model == "two_i" and not args.no_extra_configs and world == 1:
+        dm = demo_model()
+        demo = {"model": dm, "starts": demo_fit_starts(dm)}
+        if cpu is not None:
+            cpu["mcmc_demo_fit_32chains"] = cpu_demo_fit_baseline(dm, demo["starts"])
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     mh_flops, mh_flops_note = None, "skipped (--no-pmc, N>1 or no MCMC leg)"
     if world == 1 and not args.no_pmc and not args.mcmc_only:
@@ -804,6 +972,8 @@ def main():
         extra["C4"] = c4_leg(args, R, T, P)
     if world == 1 and not args.no_extra_configs:
         extra.update(extra_configs(args, R, T, P))
+        if demo is not None:
+            extra["MCMC-demo-fit-32chains"] = demo_fit_leg(demo, cpu)
 
     if rank == 0:
         line = {
@@ -815,13 +985,17 @@ def main():
             "config": {"workload": f"{args.model} {args.method} trajectory-mode integrate + fused chi",
                        "walkers_per_gpu": Wl, "walkers_total": Wl * world, "states": S, "times": T,
                        "method": args.method, "rk4_substeps": 1,
-                       "tolerance": "vs tight odeint: rtol 1e-6, atol 1e-6 (test-pinned)",
+                       "tolerance": tolerance_of(args.model, args.method, 1, fp.rtol, fp.atol),
                        "stores": "cached" if args.cached_stores else "nontemporal",
                        "kernel": ran, "kernel_choice": kernel, "kernel_tune_ms": tune, "xcd": args.xcd,
                        "parallelism": f"walker-shard x{world}",
                        "launch": "torchrun, one rank per GPU" if world > 1 else "single process"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_of(traffic, ran, args.method),
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "frac_wall": bytes_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS,
+                         "frac_note": "frac: the timed region's event span per launch (kernel time); frac_wall: "
+                                      "ms_per_step, the wall time value is computed from (host launch gaps included)",
+                         "traffic": traffic_of(traffic, ran, args.method),
                          "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_s * 1e3, "kernel_ms_note": "timed-region event span / steps",
                          "kernel_ms_per_dispatch": kern_dispatch_ms, "bytes_per_launch": bytes_launch,

@@ -99,7 +99,9 @@ enum {
   OE_HOST_PTRS = 1u, /* buffers are host memory */
   OE_ASYNC = 2u,     /* do not synchronize before returning (device pointers only) */
   OE_NT_STORES = 4u, /* non-temporal trajectory stores */
-  OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel, 2 store waves (built-in models, W even) */
+  OE_PIPE = 8u,      /* RK4 trajectories via the producer/consumer kernel, 2 store waves (built-in models, W even);
+                       OE_METHOD_DOPRI5 trajectories (built-in models, S <= 6, one lane per walker): the
+                       store-wave kernel (dense output + row stores off the compute waves; same bits) */
   OE_HALF_WAVES = 16u, /* RK4: 32 walkers per wavefront (twice the waves; same results). Chosen
                          automatically for trajectories with S >= 5 at <= 1 wave per SIMD. */
   /* 32u: reserved (was an experimental split-wave layout, measured slower and removed) */
@@ -303,6 +305,19 @@ int oe_comm_set_stream(oe_comm* comm, void* hip_stream);
  * OE_ASYNC (do not synchronize the stream before returning). */
 int oe_allgather_samples(oe_comm* comm, int64_t rows, const double* block, const int64_t* counts, double* out,
                          uint32_t flags);
+/* The two data movements of oe_allgather_samples, callable without a communicator (one
+ * device; tests drive the n-rank layout with a synthetic gathered buffer):
+ *   oe_pool_pad:      block [rows][count] -> padded [rows][cmax] (zeros beyond count), the
+ *                     send block of a rank with fewer walkers than the largest;
+ *   oe_pool_relayout: the collective's rank-major result gathered [n_ranks][rows][cmax]
+ *                     (cmax = max counts) -> out [rows][sum(counts)], rank r's walkers at
+ *                     columns sum(counts[:r]) .. + counts[r] (global walker order).
+ * Device pointers; hip_stream NULL = the null stream; synchronous unless OE_ASYNC.  Errors
+ * read with oe_comm_last_error(NULL). */
+int oe_pool_pad(int64_t rows, const double* block, int64_t count, int64_t cmax, double* padded, void* hip_stream,
+                uint32_t flags);
+int oe_pool_relayout(int32_t n_ranks, int64_t rows, const int64_t* counts, const double* gathered, double* out,
+                     void* hip_stream, uint32_t flags);
 
 /* Device time (ms) of the kernel launches of the last oe_integrate / oe_mh_run,
  * from HIP events recorded on the context's stream around them (waits for them). */

@@ -53,6 +53,8 @@ EXPORTED = (
     "oe_comm_last_error",
     "oe_comm_set_stream",
     "oe_allgather_samples",
+    "oe_pool_pad",
+    "oe_pool_relayout",
     "oe_last_variant",
     "oe_tune_times",
     "oe_last_mh_depth",
@@ -180,6 +182,10 @@ def load_library(path: str | None = None):
         lib.oe_comm_set_stream.argtypes = [vp, vp]
         lib.oe_allgather_samples.restype = C.c_int
         lib.oe_allgather_samples.argtypes = [vp, i64, vp, vp, vp, u32]
+        lib.oe_pool_pad.restype = C.c_int
+        lib.oe_pool_pad.argtypes = [i64, vp, i64, i64, vp, vp, u32]
+        lib.oe_pool_relayout.restype = C.c_int
+        lib.oe_pool_relayout.argtypes = [i32, i64, vp, vp, vp, vp, u32]
         lib.oe_last_variant.restype = C.c_int
         lib.oe_last_variant.argtypes = [vp, C.POINTER(i32)]
         lib.oe_last_mh_depth.restype = C.c_int
@@ -303,6 +309,26 @@ def comm_unique_id() -> bytes:
     if rc != OE_OK:
         raise RuntimeError(f"oe_comm_unique_id failed ({rc}): {lib.oe_comm_last_error(None).decode()}")
     return bytes(buf)
+
+
+def pool_pad(rows: int, block_ptr, count: int, cmax: int, padded_ptr, stream: int = 0, flags: int = 0):
+    """``oe_pool_pad``: a rank's block [rows][count] padded to [rows][cmax] (device)."""
+    lib = load_library()
+    rc = lib.oe_pool_pad(int(rows), block_ptr, int(count), int(cmax), padded_ptr, C.c_void_p(int(stream)), int(flags))
+    if rc != OE_OK:
+        raise RuntimeError(f"oe_pool_pad failed ({rc}): {lib.oe_comm_last_error(None).decode()}")
+
+
+def pool_relayout(counts, rows: int, gathered_ptr, out_ptr, stream: int = 0, flags: int = 0):
+    """``oe_pool_relayout``: the rank-major gathered [n][rows][max(counts)] -> [rows][sum(counts)]
+    in global walker order (device)."""
+    import numpy as np
+    lib = load_library()
+    cnt = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
+    rc = lib.oe_pool_relayout(len(cnt), int(rows), C.c_void_p(cnt.ctypes.data), gathered_ptr, out_ptr,
+                              C.c_void_p(int(stream)), int(flags))
+    if rc != OE_OK:
+        raise RuntimeError(f"oe_pool_relayout failed ({rc}): {lib.oe_comm_last_error(None).decode()}")
 
 
 class Comm:

@@ -97,12 +97,24 @@ __device__ __forceinline__ double norm_max(double c, const double (&v)[S], const
 }
 
 // scipy's change_D for a step-size change by `factor` at order q, in two stages:
-// E = R(q, factor)^T D, then D = U^T E (the same product as (RU)^T D, U exact).  State by
-// state, so only one state's E is live (the R coefficients are recomputed per state: the
-// same values every time).
+// E = R(q, factor)^T D, then D = U^T E (the same product as (RU)^T D, U exact).  The R
+// coefficients r[m][i] = R[i][m] once (wave-uniform), then state by state, so only one
+// state's E is live.
 template <int S>
 __device__ __forceinline__ void change_D(double (&D)[kRows][S], int q, double factor) {
   const cptr<double> U = kconst(&kU[0][0]), inv_i = kconst(kInvI);
+  double r[kMaxQ + 1][kMaxQ + 1];
+#pragma unroll
+  for (int m = 1; m <= kMaxQ; ++m) {
+    if (m > q) break;
+    double v = 1.0;
+#pragma unroll
+    for (int i = 1; i <= kMaxQ; ++i) {
+      if (i > q) break;
+      v = v * (((double)(i - 1) - factor * (double)m) * inv_i[i]);
+      r[m][i] = v;
+    }
+  }
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     double E[kMaxQ + 1];
@@ -110,12 +122,11 @@ __device__ __forceinline__ void change_D(double (&D)[kRows][S], int q, double fa
 #pragma unroll
     for (int m = 1; m <= kMaxQ; ++m) {
       if (m > q) break;
-      double r = 1.0, e = D[0][s];
+      double e = D[0][s];
 #pragma unroll
       for (int i = 1; i <= kMaxQ; ++i) {
         if (i > q) break;
-        r = r * (((double)(i - 1) - factor * (double)m) * inv_i[i]);
-        e = fma(r, D[i][s], e);
+        e = fma(r[m][i], D[i][s], e);
       }
       E[m] = e;
     }
@@ -323,6 +334,9 @@ __device__ __forceinline__ void bdf_step(const DevProblem& pb, BdfState<M::S>& s
     return;
   }
   // accepted: differences, this lane's grid points, lanes that reach t_end leave
+#ifdef OE_BDF_TRACE
+  if (st.live && blockIdx.x == 0 && threadIdx.x == 0) printf("ACC Q=%d t=%.17g h=%.17g niter=%d\n", Q, st.t, h, niter);
+#endif
   ++st.neq;
   st.fresh = false;
   const bool select = st.neq >= Q + 1;  // wave-uniform: order and step selection after this step
@@ -342,6 +356,9 @@ __device__ __forceinline__ void bdf_step(const DevProblem& pb, BdfState<M::S>& s
     ++st.nst;
     double yo[S];
     const double* times = pb.times;
+    double rden[Q + 1];  // 1/(j·h): one division per order per step, not per grid point
+#pragma unroll
+    for (int j = 1; j <= Q; ++j) rden[j] = 1.0 / ((double)j * h);
     while (st.i < pb.T && times[st.i] <= tn) {
       const double ti = times[st.i];
       double prod = 1.0;
@@ -349,11 +366,14 @@ __device__ __forceinline__ void bdf_step(const DevProblem& pb, BdfState<M::S>& s
       for (int s = 0; s < S; ++s) yo[s] = st.D[0][s];
 #pragma unroll
       for (int j = 1; j <= Q; ++j) {
-        const double x = (ti - (tn - (double)(j - 1) * h)) / ((double)j * h);
+        const double x = (ti - (tn - (double)(j - 1) * h)) * rden[j];
         prod = prod * x;
 #pragma unroll
         for (int s = 0; s < S; ++s) yo[s] = fma(st.D[j][s], prod, yo[s]);
       }
+#ifdef OE_BDF_TRACE
+      if (blockIdx.x == 0 && threadIdx.x == 0) printf("EMIT i=%d y1=%.17g\n", st.i, yo[1]);
+#endif
       emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, a);
       ++st.i;
       st.nst = 0;

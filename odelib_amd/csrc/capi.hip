@@ -108,7 +108,7 @@ struct oe_ctx {
     const Entry* e;
     int64_t W;
     int32_t T, substeps;
-    uint32_t mode;  // nt | xcd flags
+    uint32_t mode;  // nt | xcd flags | OE_HALF_WAVES (the default kernel a candidate must beat)
     int32_t variant;
     double ms[OE_KERNEL_COUNT - 1];
   };
@@ -275,7 +275,7 @@ std::vector<oe_ctx::Tuned> g_tuned;
 // process: another context on the device reuses the choice).
 int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32_t flags, int dflt,
              oe_ctx::Tuned* out) {
-  const uint32_t mode = (nt ? 1u : 0u) | (flags & (OE_NO_XCD_REMAP | OE_XCD_RANGES));
+  const uint32_t mode = (nt ? 1u : 0u) | (flags & (OE_NO_XCD_REMAP | OE_XCD_RANGES | OE_HALF_WAVES));
   const bool shared = e->rtc == nullptr;
   auto match = [&](const oe_ctx::Tuned& t) {
     return t.device == c->device && t.e == e && t.W == ia.W && t.T == c->dp.T && t.substeps == c->dp.substeps &&
@@ -314,7 +314,9 @@ int tune_rk4(oe_ctx* c, const Entry* e, const IntegrateArgs& ia, bool nt, uint32
   if (rc) return rc;
   // launches per measurement: ~15 ms of work, 4..16 launches
   const int per = std::max(4, std::min(16, (int)std::ceil(15.0 / std::max(ms, 1e-3f))));
-  for (double settled = ms; settled < 60.0;) {
+  // (bounded by a launch count too: a clock that reports no elapsed time must not hang the call)
+  double settled = ms;
+  for (int n = 0; settled < 60.0 && n < 64; ++n) {
     rc = batch(dflt, per, &ms);
     if (rc) return rc;
     settled += ms;
@@ -868,6 +870,14 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   if (timing) OE_HIP(c, hipEventRecord(c->ev0, c->stream));
   if (rk4_traj) {
     OE_HIP(c, launch_rk4_traj(c, e, ia, variant, nt, flags));
+  } else if (c->method == OE_METHOD_DOPRI5 && ia.traj && !e->rtc && e->dopri5_piped[0] && (flags & OE_PIPE) &&
+             (e->split_lanes == 0 || (flags & OE_NO_SPLIT))) {
+    // DOPRI5 trajectories through store waves (k_integrate_dopri5_piped): 4 compute + 4 store
+    // waves per 256 walkers, blocks dealt to the XCDs in runs of 512 walkers as k_integrate's
+    const dim3 grid((unsigned)((W + 255) / 256)), block(512);
+    ia.half = 0;
+    ia.xcd_remap = xcd_remap_of(flags, grid, 256);
+    e->dopri5_piped[nt ? 1 : 0](c->dp, ia, grid, block, c->stream);
   } else if (c->method == OE_METHOD_DOPRI5 && !e->rtc && e->split_lanes > 0 && !(flags & OE_NO_SPLIT)) {
     // wide chain models: one walker over K adjacent lanes (split.cuh), blocks of 256/K
     // walkers dealt to the XCDs in runs of 512 walkers as the one-lane kernel's
@@ -1029,6 +1039,10 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       depth = std::min(a->speculate, 16);
     }
     if (depth < 2 || ((int64_t(1) << depth) - 1) * W > kMaxWalkers) depth = 0;
+    // the tree buffer ((2^d - 1)·W·(P + 2) doubles) within 4 GiB, like the draw buffers'
+    // budget: a deeper explicit request is cut to the deepest tree that fits
+    while (depth >= 2 && (double)((int64_t(1) << depth) - 1) * (double)W * (8.0 * (P + 2) + 4.0) > 4294967296.0) --depth;
+    if (depth < 2) depth = 0;
   }
   c->last_mh_depth = depth;
   MHTreeArgs ta{};
@@ -1043,9 +1057,18 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
         c->tree = nullptr;
         c->tree_bytes = 0;
       }
-      OE_HIP(c, hipMalloc(&c->tree, bytes));
-      c->tree_bytes = bytes;
+      if (hipMalloc(&c->tree, bytes) != hipSuccess) {  // out of memory: one iteration per step
+        (void)hipGetLastError();
+        c->tree = nullptr;
+        depth = 0;
+        c->last_mh_depth = 0;
+      } else {
+        c->tree_bytes = bytes;
+      }
     }
+  }
+  if (depth) {
+    const int64_t nodes = (int64_t(1) << depth) - 1;
     double* b = static_cast<double*>(c->tree);
     ta.node_th = b;
     ta.node_chi = b + (size_t)(nodes * W) * P;

@@ -104,9 +104,62 @@ struct DevGuard {
   }
 };
 
+// the data movement around the collective, usable without a communicator
+// (oe_pool_pad / oe_pool_relayout): one rank's block padded to [rows][cmax] ...
+hipError_t pad_block(int64_t rows, const double* block, int64_t cnt, int64_t cmax, double* padded, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(padded, 0, sizeof(double) * (size_t)rows * (size_t)cmax, s);
+  if (e != hipSuccess || cnt == 0) return e;
+  return hipMemcpy2DAsync(padded, sizeof(double) * cmax, block, sizeof(double) * cnt, sizeof(double) * cnt,
+                          (size_t)rows, hipMemcpyDeviceToDevice, s);
+}
+
+// ... and the gathered rank-major [n][rows][cmax] laid out walker-minor [rows][n_total] in
+// global walker order (rank r's walkers at columns off[r] .. off[r] + counts[r]): one strided
+// copy per rank
+hipError_t relayout(int n, int64_t rows, const int64_t* counts, const int64_t* off, int64_t cmax,
+                    const double* gathered, double* out, hipStream_t s) {
+  for (int r = 0; r < n; ++r) {
+    if (counts[r] == 0) continue;
+    const hipError_t e = hipMemcpy2DAsync(out + off[r], sizeof(double) * off[n], gathered + (size_t)r * rows * cmax,
+                                          sizeof(double) * cmax, sizeof(double) * counts[r], (size_t)rows,
+                                          hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 }  // namespace
 
 extern "C" {
+
+int oe_pool_pad(int64_t rows, const double* block, int64_t count, int64_t cmax, double* padded, void* hip_stream,
+                uint32_t flags) {
+  if (rows < 0 || count < 0 || cmax < count || (rows > 0 && cmax > 0 && !padded) || (rows > 0 && count > 0 && !block))
+    return comm_fail(nullptr, OE_ERR_ARG, "oe_pool_pad: need 0 <= count <= cmax and device buffers");
+  if (rows == 0 || cmax == 0) return OE_OK;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  OE_HIPC(nullptr, pad_block(rows, block, count, cmax, padded, s));
+  if (!(flags & OE_ASYNC)) OE_HIPC(nullptr, hipStreamSynchronize(s));
+  return OE_OK;
+}
+
+int oe_pool_relayout(int32_t n_ranks, int64_t rows, const int64_t* counts, const double* gathered, double* out,
+                     void* hip_stream, uint32_t flags) {
+  if (n_ranks < 1 || rows < 0 || !counts) return comm_fail(nullptr, OE_ERR_ARG, "oe_pool_relayout: bad arguments");
+  std::vector<int64_t> off(n_ranks + 1, 0);
+  int64_t cmax = 0;
+  for (int r = 0; r < n_ranks; ++r) {
+    if (counts[r] < 0) return comm_fail(nullptr, OE_ERR_ARG, "oe_pool_relayout: negative count");
+    off[r + 1] = off[r] + counts[r];
+    cmax = std::max(cmax, counts[r]);
+  }
+  if (rows == 0 || cmax == 0) return OE_OK;
+  if (!gathered || !out) return comm_fail(nullptr, OE_ERR_ARG, "oe_pool_relayout: null buffer");
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  OE_HIPC(nullptr, relayout(n_ranks, rows, counts, off.data(), cmax, gathered, out, s));
+  if (!(flags & OE_ASYNC)) OE_HIPC(nullptr, hipStreamSynchronize(s));
+  return OE_OK;
+}
 
 int oe_comm_unique_id(uint8_t* id, int32_t id_bytes) {
   if (!id || id_bytes != OE_COMM_ID_BYTES) return comm_fail(nullptr, OE_ERR_ARG, "oe_comm_unique_id: need a 128-byte buffer");
@@ -204,21 +257,12 @@ int oe_allgather_samples(oe_comm* c, int64_t rows, const double* block, const in
   const double* send = block;
   if (cnt < cmax) {  // pad this rank's block to [rows][cmax]
     double* pad = reinterpret_cast<double*>(base + (n == 1 ? 0 : blk * (size_t)n));
-    OE_HIPC(c, hipMemsetAsync(pad, 0, blk, s));
-    if (cnt > 0)
-      OE_HIPC(c, hipMemcpy2DAsync(pad, sizeof(double) * cmax, block, sizeof(double) * cnt, sizeof(double) * cnt,
-                                  (size_t)rows, hipMemcpyDeviceToDevice, s));
+    OE_HIPC(c, pad_block(rows, block, cnt, cmax, pad, s));
     send = pad;
   }
   OE_NCCL(c, R.all_gather(send, gathered, (size_t)rows * (size_t)cmax, ncclFloat64, c->nc, s));
-  if (n > 1) {
-    // rank-major [n][rows][cmax] -> walker-minor [rows][n_total], rank r at column off[r]
-    for (int r = 0; r < n; ++r)
-      if (counts[r] > 0)
-        OE_HIPC(c, hipMemcpy2DAsync(out + off[r], sizeof(double) * off[n], gathered + (size_t)r * rows * cmax,
-                                    sizeof(double) * cmax, sizeof(double) * counts[r], (size_t)rows,
-                                    hipMemcpyDeviceToDevice, s));
-  }
+  // rank-major [n][rows][cmax] -> walker-minor [rows][n_total], rank r at column off[r]
+  if (n > 1) OE_HIPC(c, relayout(n, rows, counts, off.data(), cmax, gathered, out, s));
   if (!(flags & OE_ASYNC)) OE_HIPC(c, hipStreamSynchronize(s));
   return OE_OK;
 }

@@ -27,6 +27,7 @@ struct Entry {
   // S > kStiffRegS
   IntegrateLaunch integrate[kMethods][2][2];
   IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > OE_PIPE_MAX_S
+  IntegrateLaunch dopri5_piped[2];  // [nt]: DOPRI5 trajectories through store waves; null when S > 6
   MHLaunch mh[kMethods];
   MHTreeLaunch mh_tree[kMethods];  // speculative MH rounds (k_mh_tree); the resolve kernel is shared
   StiffWaveLaunch stiff_wave[2][2];  // [traj][nt]: S > kStiffRegS stiff redo, one wave per walker
@@ -68,6 +69,10 @@ void launch_integrate(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim
 template <class M, bool NT, int NSW>
 void launch_rk4_piped(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_integrate_rk4_piped<M, NT, NSW>), g, b, 0, s, pb, ia);
+}
+template <class M, bool NT>
+void launch_dopri5_piped(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_integrate_dopri5_piped<M, NT>), g, b, 0, s, pb, ia);
 }
 template <class M, int METHOD>
 void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
@@ -149,6 +154,10 @@ Entry make_entry(int32_t model_id) {
     fill_method<M, kRosenbrock>(e);
   }
   if constexpr (M::S <= kStiffRegS) fill_method<M, kBdf>(e);
+  if constexpr (M::S <= 8 && dp_pipe_slots<M::S>() >= 2) {  // a slot ring of >= 2 steps fits (S <= 6)
+    e.dopri5_piped[0] = launch_dopri5_piped<M, false>;
+    e.dopri5_piped[1] = launch_dopri5_piped<M, true>;
+  }
   if constexpr (M::S > kStiffRegS && M::S <= kStiffMaxS) {
     e.stiff_wave[0][0] = launch_stiff_wave<M, false, false>;
     e.stiff_wave[0][1] = launch_stiff_wave<M, false, false>;

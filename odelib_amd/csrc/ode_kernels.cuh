@@ -517,17 +517,82 @@ __device__ __forceinline__ double inv_fifth_root_uniform(double x, cptr<double> 
 // AUTO: Hairer's stiffness test on every accepted step (h·|λ| estimated from the last two
 // stages, ≥ 3.25 on 15 accepted steps in a row evicts the lane, as does the step
 // budget); returns whether this (active) lane was evicted, i.e. needs the stiff method.
+// ---- DOPRI5 trajectory output through store waves (k_integrate_dopri5_piped) ----------
+// A compute wave publishes, per accepted step that reaches a grid time, the step's dense-
+// output coefficients (y, ydf, bsp, r4, r5, ynew: 6·S doubles per lane) and the uniform
+// (t, t_new, 1/h) into its own LDS slot ring; its store wave evaluates the dense output at
+// every grid time of the step (the compute wave's own operations, so the same bits), tracks
+// the running minimum and writes the rows with NT buffer stores.  The two waves synchronise
+// through a produced / consumed counter pair per compute wave — no barrier couples the
+// compute waves, whose step sequences differ.  Observed rows are still evaluated by the
+// compute wave (the likelihood), every other row never costs it an instruction.
+constexpr int kDpPipeFields = 6;  // y, ydf, bsp, r4, r5, ynew
+template <int S>
+constexpr int dp_pipe_slots() {  // slots per compute wave: 4 compute waves in 150 KiB of LDS
+  return (150 * 1024) / (4 * (kDpPipeFields * S * 64 * 8 + 32)) < 8 ? (150 * 1024) / (4 * (kDpPipeFields * S * 64 * 8 + 32)) : 8;
+}
+template <int S>
+struct DpPipe {
+  double* ring;            // [R][6·S][64] this wave's slots
+  double* uni;             // [R][4]: t, t_new, 1/h
+  volatile int* produced;  // slots published by the compute wave
+  volatile int* consumed;  // slots released by the store wave
+  int lane, R, n, cons_seen;
+};
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// wait for a free slot, fill it, publish it
+template <int S>
+__device__ __forceinline__ void dp_pipe_publish(DpPipe<S>& pp, double t, double tn, double rh, const double (&y)[S],
+                                                const double (&ydf)[S], const double (&bsp)[S], const double (&r4)[S],
+                                                const double (&r5)[S], const double (&yn)[S]) {
+  while (pp.n - pp.cons_seen >= pp.R) {  // ring full: see how far the store wave is
+    pp.cons_seen = *pp.consumed;
+    if (pp.n - pp.cons_seen >= pp.R) __builtin_amdgcn_s_sleep(1);
+  }
+  const int slot = pp.n % pp.R;
+  double* f = pp.ring + (size_t)slot * kDpPipeFields * S * 64 + pp.lane;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    f[(0 * S + s) * 64] = y[s];
+    f[(1 * S + s) * 64] = ydf[s];
+    f[(2 * S + s) * 64] = bsp[s];
+    f[(3 * S + s) * 64] = r4[s];
+    f[(4 * S + s) * 64] = r5[s];
+    f[(5 * S + s) * 64] = yn[s];
+  }
+  if (pp.lane == 0) {
+    pp.uni[slot * 4 + 0] = t;
+    pp.uni[slot * 4 + 1] = tn;
+    pp.uni[slot * 4 + 2] = rh;
+  }
+  lds_fence();  // the slot's data before the counter
+  ++pp.n;
+  if (pp.lane == 0) *pp.produced = pp.n;
+}
+
 // RESUME (auto, S <= kStiffRegS): an evicted lane is handed over to BDF — its state at the
 // eviction point goes to *rs and the return value says so — instead of being redone from t0.
-template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false, bool SLOW_REDO = false, bool RESUME = false>
+// PIPE (trajectory mode, S <= 8, k_integrate_dopri5_piped): the rows go through *pp to the
+// store wave (same values, same minimum), the compute wave only evaluates observed rows.
+template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false, bool SLOW_REDO = false, bool RESUME = false,
+          bool PIPE = false>
 __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, uint32_t off, bool active, Acc& a,
-                                                 Resume<M::S>* rs = nullptr) {
+                                                 Resume<M::S>* rs = nullptr, DpPipe<M::S>* pp = nullptr) {
   using namespace dp;
   constexpr int S = M::S;
+  static_assert(!PIPE || (TRAJ && S <= 8 && !AUTO), "the piped output is DOPRI5 trajectory mode's, S <= 8");
   int k = 0;
-  emit<S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
+  if constexpr (PIPE) {  // row 0 = the initial state: a slot whose end time is times[0]
+    const double t00 = kconst(pb.times)[0];
+    dp_pipe_publish<S>(*pp, t00, t00, 0.0, y, y, y, y, y, y);
+    observe<S>(pb, 0, y, k, a);
+  } else {
+    emit<S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
+  }
   const cptr<double> times = kconst(pb.times);
   const double t0 = times[0];
   const double tend = times[pb.T - 1];
@@ -701,6 +766,9 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
           for (int s = 0; s < S; ++s) { yn[s] = __builtin_nan(""); k7[s] = __builtin_nan(""); }
         }
       }
+      if constexpr (RESUME) {  // every lane handed over (or idle): nothing left for this pass
+        if (__ballot(!dead) == 0ull) break;
+      }
       const double tn = last ? tend : t + h;
       // Dense output for every grid point in (t, tn] from Hairer's coefficients
       // ydf, bsp, r4, r5.  Trajectory mode: formed eagerly once per accepted step (a grid
@@ -725,6 +793,11 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
         }
       }
       if constexpr (!kLean) {
+        // PIPE: a step that reaches a grid time hands its coefficients to the store wave
+        if constexpr (PIPE) {
+          if (t_i <= tn) dp_pipe_publish<S>(*pp, t, tn, rh, y, ydf, bsp, r4, r5, yn);
+        }
+        constexpr bool kAll = TRAJ && !PIPE;  // every grid point evaluated here
         // grid points strictly inside the step: dense output (no per-point test for the
         // end point, whose row is the new state itself: handled after the loop, so the
         // dense values go straight to the store registers)
@@ -733,7 +806,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
         while (t_i < tn) {
           const double ti = t_i;
           t_i = *tnext++;  // times[i + 1]: issued now, used next iteration
-          if (TRAJ || i == nxt) {
+          if (kAll || i == nxt) {
             const double th = (ti - t) * rh;
             const double th1 = 1.0 - th;
             double yo[S];
@@ -741,27 +814,27 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
             for (int s = 0; s < S; ++s)
               yo[s] = fma(th, fma(th1, fma(th, fma(th1, r5[s], r4[s]), bsp[s]), ydf[s]), y[s]);
             // (an evicted lane's state is NaN, so its dense output is NaN already)
-            store_row_at<S, TRAJ, NT>(trow, yo, W, off, active, a);
+            if constexpr (!PIPE) store_row_at<S, TRAJ, NT>(trow, yo, W, off, active, a);
             if (i == nxt) {
               observe_next<S>(pb, i, yo, k, nxt, a);
               t_obs = times[nxt < pb.T ? nxt : pb.T];
             }
           }
           ++i;
-          if constexpr (TRAJ) trow += S * W;
+          if constexpr (kAll) trow += S * W;
           nst = 0;
         }
         if (t_i == tn) {  // a grid point on the step's end
           t_i = *tnext++;
-          if (TRAJ || i == nxt) {
-            store_row_at<S, TRAJ, NT>(trow, yn, W, off, active, a);
+          if (kAll || i == nxt) {
+            if constexpr (!PIPE) store_row_at<S, TRAJ, NT>(trow, yn, W, off, active, a);
             if (i == nxt) {
               observe_next<S>(pb, i, yn, k, nxt, a);
               t_obs = times[nxt < pb.T ? nxt : pb.T];
             }
           }
           ++i;
-          if constexpr (TRAJ) trow += S * W;
+          if constexpr (kAll) trow += S * W;
           nst = 0;
         }
       } else {
@@ -839,8 +912,15 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
         double yo[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
-        for (; i < pb.T; ++i)
-          if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
+        if constexpr (PIPE) {  // one slot of NaN coefficients reaching t = +inf: NaN rows to the end
+          dp_pipe_publish<S>(*pp, t, __builtin_inf(), 0.0, yo, yo, yo, yo, yo, yo);
+          for (; i < pb.T; ++i) observe<S>(pb, i, yo, k, a);
+        } else if constexpr (RESUME) {
+          // every lane handed over (or idle): the BDF pass writes their rows
+        } else {
+          for (; i < pb.T; ++i)
+            if (grid_needs_emit<S, TRAJ>(pb, i, k)) emit<S, TRAJ, NT>(pb, i, yo, traj, W, off, active, k, a);
+        }
         break;
       }
       if (h < hmin) h = fmin(1e-3 * span, tend - t);
@@ -998,6 +1078,104 @@ __global__ void __launch_bounds__(256)
     if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
     if (ia.ssres) ia.ssres[w] = a.ssres;
     if (ia.status) ia.status[w] = finish(a);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Kernel 1c: DOPRI5 trajectory mode with store waves (C2; S <= 8).
+//
+// One workgroup = 4 COMPUTE waves (256 walkers, one per lane, the lockstep DOPRI5 of
+// k_integrate with the same step sequences) + 4 STORE waves, store wave c serving compute
+// wave c through that wave's slot ring (DpPipe): the dense output at the non-observed grid
+// times, the running minimum and the row stores leave the compute wave, whose VALU issue
+// sets the kernel time at one wave per SIMD.  Per-wave counters, no
+// phase barrier; one workgroup barrier at the end merges the store waves' minima into the
+// status bits.  Same outputs as k_integrate<M, DOPRI5, true, NT>, bit for bit.
+// ---------------------------------------------------------------------------------
+template <class M, bool NT>
+__global__ void __launch_bounds__(512) k_integrate_dopri5_piped(const DevProblem pb, const IntegrateArgs ia) {
+  constexpr int S = M::S;
+  constexpr int PMAX = kPmax<M>;
+  constexpr int R = dp_pipe_slots<S>();
+  static_assert(R >= 2, "slot ring too small");
+  __shared__ double ring[4][R][kDpPipeFields * S * 64];
+  __shared__ double uni[4][R][4];
+  __shared__ int produced[4], consumed[4];
+  __shared__ double ymin_sh[4][64];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int c = wave & 3;  // the compute wave (and its store wave)
+  if (threadIdx.x < 4) { produced[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
+  __syncthreads();
+  const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x, ia.xcd_remap) : (int64_t)blockIdx.x;
+  const int64_t gw = blk * 256 + c * 64 + lane;
+  const bool active = gw < ia.W;
+  const int64_t w = active ? gw : ia.W - 1;
+  const int64_t W = ia.W;
+  const int T = pb.T;
+  if (wave < 4) {
+    // ------------------------------ compute waves ------------------------------
+    double y[S], p[PMAX];
+#pragma unroll
+    for (int s = 0; s < S; ++s) y[s] = ia.y0[(int64_t)s * W + w];
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
+    Acc a = acc_init();
+    DpPipe<S> pp{&ring[c][0][0], &uni[c][0][0], &produced[c], &consumed[c], lane, R, 0, 0};
+    integrate_dopri5<M, PMAX, true, NT, false, false, false, true>(pb, y, p, ia.traj, W, (uint32_t)w * 8u, active, a,
+                                                                 nullptr, &pp);
+    __syncthreads();  // the store waves' minima
+    a.ymin = min_raw(a.ymin, ymin_sh[c][lane]);
+    if (active) {
+      if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
+      if (ia.ssres) ia.ssres[w] = a.ssres;
+      if (ia.status) ia.status[w] = finish(a);
+    }
+  } else {
+    // ------------------------------ store waves --------------------------------
+    const double* times = pb.times;
+    const uint32_t off = (uint32_t)w * 8u;
+    const uint32_t row_bytes = (uint32_t)(S * W * 8);
+    Acc a = acc_init();  // only its running minimum is used
+    int i = 0;
+    for (int n = 0; i < T; ++n) {
+      while (*(volatile int*)&produced[c] <= n) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+      const int slot = n % R;
+      const double* f = &ring[c][slot][0] + lane;
+      const double t = uni[c][slot][0], tn = uni[c][slot][1], rh = uni[c][slot][2];
+      double y[S], ydf[S], bsp[S], r4[S], r5[S], yn[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        y[s] = f[(0 * S + s) * 64];
+        ydf[s] = f[(1 * S + s) * 64];
+        bsp[s] = f[(2 * S + s) * 64];
+        r4[s] = f[(3 * S + s) * 64];
+        r5[s] = f[(4 * S + s) * 64];
+        yn[s] = f[(5 * S + s) * 64];
+      }
+      lds_fence();  // the slot is read: release it
+      if (lane == 0) *(volatile int*)&consumed[c] = n + 1;
+      double ti = times[i];
+      while (ti < tn) {  // the compute wave's dense output, operation for operation
+        const double th = (ti - t) * rh;
+        const double th1 = 1.0 - th;
+        double yo[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          yo[s] = fma(th, fma(th1, fma(th, fma(th1, r5[s], r4[s]), bsp[s]), ydf[s]), y[s]);
+        store_row_at<S, true, NT>(ia.traj + (int64_t)i * S * W, yo, W, off, active, a);
+        ++i;
+        ti = times[i];  // times[T] is the +inf sentinel
+      }
+      if (ti == tn) {
+        store_row_at<S, true, NT>(ia.traj + (int64_t)i * S * W, yn, W, off, active, a);
+        ++i;
+      }
+    }
+    (void)row_bytes;
+    ymin_sh[c][lane] = a.ymin;
+    __syncthreads();
   }
 }
 

@@ -57,6 +57,8 @@ def native_comm(device: int, group=None):
     caller does the same with any channel."""
     import torch.distributed as dist
     from . import _native as N
+    if not (dist.is_available() and dist.is_initialized()):  # one process: a 1-rank communicator
+        return N.Comm(device, 1, 0, N.comm_unique_id())
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     obj = [N.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
@@ -87,8 +89,14 @@ def sharded_mh(engine, theta_all, y0_all, nits: int, burnin: int, walk_mask, ini
     ``group`` (each rank: its shard on its own device via ``engine``), Philox draws, and
     return the pooled posterior samples [kept][P+5][W_total] (identical on all ranks).
     ``speculate``: each rank's speculative MH rounds (``Engine.mh_run``; on for shards too
-    small to fill their device) — the draws are keyed by global walker id and iteration, so
-    the chains are those of one sequential launch either way."""
+    small to fill their device).  The draws are keyed by global walker id and iteration, so
+    with RK4 (every lane integrates alone) the pooled chains are bitwise those of one
+    sequential launch for any rank count.  With DOPRI5 / 'auto' a proposal shares its step
+    size with its lockstep group, which the sharding and the speculation depth (picked from
+    each rank's shard size and CU count) change: chi moves at the tolerance level, and a
+    decision whose margin |accp - u| is below ~1e-7 can flip (none in 576 restated chains,
+    tests/test_rkref_oracle.py::test_c_speculative_decision_agreement_over_many_chains) — the
+    posterior is then the same distribution, not the same bits."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     W = int(np.asarray(theta_all).shape[1]) if not hasattr(theta_all, "shape") else int(theta_all.shape[1])

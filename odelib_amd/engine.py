@@ -399,7 +399,16 @@ class Engine:
         a.step_sd = float(step_sd)
         a.walk_mask = wm.ctypes.data
         a.init_param = ip.ctypes.data
-        a.speculate = -1 if speculate in ("auto", True) else int(speculate or 0)
+        # "auto" / True: the library's depth rule; an integer (False = 0) is the depth itself, and
+        # 0 or 1 means one iteration per step (ints are tested before bools: 1 == True)
+        if isinstance(speculate, str):
+            if speculate != "auto":
+                raise ValueError("speculate must be 'auto', True/False or an integer depth")
+            a.speculate = -1
+        elif speculate is True:
+            a.speculate = -1
+        else:
+            a.speculate = int(speculate or 0)
         keep = []
         if rng == "replay":
             if replay is None:

@@ -24,6 +24,7 @@
  *     the grid, for 64-lane groups sharing one step size.
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -393,6 +394,11 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
             for (int s = 0; s < S; ++s) q->yn[s] = q->k7[s] = NAN;
           }
         }
+      }
+      if (resume) { /* every lane handed over (or idle): nothing left for this pass */
+        int alive = 0;
+        for (int l = 0; l < nl; ++l) alive |= !L[l].dead;
+        if (!alive) break;
       }
       double tn = last ? tend : t + h;
       const double rh = 1.0 / h;
@@ -1125,6 +1131,7 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
         neq = 0;
       } else {
         /* accepted: differences, grid points, lanes that reach t_end leave */
+        if (getenv("RKREF_BDF_TRACE") && B[0].live) fprintf(stderr, "ACC Q=%d t=%.17g h=%.17g niter=%d\n", order, B[0].t, h, niter);
         ++neq;
         fresh = 0;
         double em = 0.0, ep = 0.0;
@@ -1141,16 +1148,18 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
           for (int j = order; j >= 0; --j)
             for (int s = 0; s < S; ++s) b->D[j][s] = b->D[j][s] + b->D[j + 1][s];
           ++b->nst;
-          double yo[MAXS];
+          double yo[MAXS], rden[BDF_MAXQ + 1];
+          for (int j = 1; j <= order; ++j) rden[j] = 1.0 / ((double)j * h);
           while (b->i < pb->T && pb->times[b->i] <= tn) {
             const double ti = pb->times[b->i];
             double prod = 1.0;
             for (int s = 0; s < S; ++s) yo[s] = b->D[0][s];
             for (int j = 1; j <= order; ++j) {
-              const double x = (ti - (tn - (double)(j - 1) * h)) / ((double)j * h);
+              const double x = (ti - (tn - (double)(j - 1) * h)) * rden[j];
               prod = prod * x;
               for (int s = 0; s < S; ++s) yo[s] = fma(b->D[j][s], prod, yo[s]);
             }
+            if (getenv("RKREF_BDF_TRACE") && l == 0) fprintf(stderr, "EMIT i=%d y1=%.17g\n", b->i, yo[1]);
             if (needs_emit(pb, tr, b->i, q->kobs)) emit(pb, b->i, yo, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
             ++b->i;
             b->nst = 0;

@@ -1,0 +1,94 @@
+"""Golden fixtures of the REFERENCE on stiff draws and near-posterior walkers (stiff.npz).
+
+Run in the build container only (needs /root/reference, read-only), after make_golden.py:
+
+    python tests/golden/make_golden_stiff.py
+
+The reference is imported exactly as make_golden.py does (pyDOE2 stub that raises,
+pandas Series.iteritems alias).  Everything below is the reference's own pipeline —
+``ModelFramework.integrate`` (odeint = LSODA, Framework.py:656, then the summation and the
+observation gather, :659-682), ``get_chi`` (masked chi, stats.py:41), ``get_Rsqrd`` and
+``get_AIC`` — at two tolerances:
+  * default: odeint's own (rtol = atol = 1.49012e-8), what a reference chain sees;
+  * tight: the same call with rtol = atol = 1e-13, by rebinding the ``odeint`` name the
+    reference's Framework module imported (``functools.partial(odeint, rtol=.., atol=..)``);
+    nothing else of the pipeline changes.
+Draws (two_i, the notebook's 4-state model):
+  * near/: 16 near-posterior walkers (theta* · exp(0.05 z), seed 1);
+  * stiff/: theta* with tau = 1e3, 1e4, 1e5, with lam = 1e3, and the notebook fit's slow
+    region (phi = 1.06e-4, the host infected within ~1e-3 time units), where LSODA runs BDF.
+Stored (numbers only): theta, trajectories [W][T][S] (states before summation), the
+predictions at the observations, chi, R², AIC, per tolerance.
+"""
+from __future__ import annotations
+
+import functools
+import os
+import sys
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from make_golden import THETA, build_model, import_reference, walker_thetas  # noqa: E402
+
+TIGHT = 1e-13
+
+
+def stiff_thetas():
+    base = [THETA["two_i"][p] for p in ("mu", "phi", "beta", "lam", "tau")]
+    rows, labels = [], []
+    for tau in (1e3, 1e4, 1e5):
+        rows.append(base[:4] + [tau])
+        labels.append(f"tau={tau:g}")
+    rows.append(base[:3] + [1e3, base[4]])
+    labels.append("lam=1e3")
+    rows.append([base[0], 1.06e-4] + base[2:])
+    labels.append("phi=1.06e-4")
+    return np.array(rows), labels
+
+
+def run(ODElib, m, TH, tol):
+    from scipy.integrate import odeint
+    fw = sys.modules["ODElib.Framework"]
+    saved = fw.odeint
+    if tol is not None:
+        fw.odeint = functools.partial(odeint, rtol=tol, atol=tol)
+    try:
+        trajs, preds, chis, rsqs, aics = [], [], [], [], []
+        for w in range(TH.shape[0]):
+            ps = list(TH[w])
+            trajs.append(m.integrate(parameters=(ps,), as_dataframe=False, sum_subpopulations=False))
+            d = m.integrate(parameters=(ps,), predict_obs=True, as_dataframe=False)
+            preds.append(np.concatenate([d[s] for s in d]))
+            c = m.get_chi(d)
+            chis.append(float(np.ma.filled(c, np.nan)))
+            rsqs.append(float(m.get_Rsqrd(d)))
+            aics.append(float(np.ma.filled(m.get_AIC(c), np.nan)))
+    finally:
+        fw.odeint = saved
+    return dict(traj=np.array(trajs), pred=np.array(preds), chi=np.array(chis), rsq=np.array(rsqs),
+                aic=np.array(aics))
+
+
+def main():
+    ODElib = import_reference()
+    warnings.filterwarnings("ignore")
+    m = build_model(ODElib, "two_i")
+    out = {}
+    near = walker_thetas("two_i", W=16, seed=1)
+    st, labels = stiff_thetas()
+    for group, TH in (("near", near), ("stiff", st)):
+        out[f"{group}/theta"] = TH
+        for tag, tol in (("default", None), ("tight", TIGHT)):
+            r = run(ODElib, m, TH, tol)
+            for k, v in r.items():
+                out[f"{group}/{tag}/{k}"] = v
+    out["stiff/labels"] = np.array(labels)
+    np.savez_compressed(os.path.join(HERE, "stiff.npz"), **out)
+    print("stiff fixtures written:", {k: v.shape for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()

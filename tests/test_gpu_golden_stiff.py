@@ -1,0 +1,70 @@
+"""The device's default integrator ('auto') and 'bdf' against the REFERENCE's own outputs on
+stiff draws and near-posterior walkers (tests/golden/stiff.npz, made by
+tests/golden/make_golden_stiff.py from /root/reference: integrate() = odeint/LSODA,
+Framework.py:656, then get_chi, stats.py:41; at odeint's default tolerance and at
+rtol = atol = 1e-13).
+
+Bars (written here):
+  * trajectories within 1e-6·|y| + 1e-6 of the reference at 1e-13 (the north star's rtol);
+  * within the reference's own error at its default tolerance: |ours − ref_default| ≤
+    |ref_default − ref_tight| + 1e-6·|y| + 1e-6;
+  * chi within rtol 1e-6 of the tight reference chi, and no further from it than 2x the
+    reference's own default-tolerance chi (+ 1e-7 relative);
+  * the same masked / unmasked pattern of the chi terms (every log(prediction) finite or not
+    as in the reference), the pattern stats.py:41 sums over.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN, product_model
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return dict(np.load(os.path.join(GOLDEN, "stiff.npz")))
+
+
+def _preds(golden, traj):
+    """observation predictions [W][37] from [T][S][W] in get_chi's order (H = S+I1+I2, V)"""
+    out = []
+    for s in golden.meta["two_i/obs_names"]:
+        idx = golden.setup[f"two_i/tidx/{s}"]
+        rows = traj[idx]  # [n][S][W]
+        out.append(rows[:, 0] + rows[:, 1] + rows[:, 2] if s == "H" else rows[:, 3])
+    return np.concatenate(out, axis=0).T
+
+
+@pytest.mark.parametrize("method", ["auto", "bdf"])
+@pytest.mark.parametrize("group", ["near", "stiff"])
+def test_device_vs_reference_fixtures(golden, fx, method, group):
+    m = product_model("two_i", method=method)
+    TH = fx[f"{group}/theta"]
+    W = TH.shape[0]
+    theta = np.ascontiguousarray(TH.T)
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    out = m.engine().integrate(y0, theta, trajectory=True)
+    traj = out["traj"].cpu().numpy()           # [T][S][W]
+    chi = out["chi"].cpu().numpy()
+    st = out["status"].cpu().numpy()
+    assert not (st & 5).any(), st               # nothing abandoned or non-finite
+    ref_t = fx[f"{group}/tight/traj"]           # [W][T][S]
+    ref_d = fx[f"{group}/default/traj"]
+    for w in range(W):
+        ours = traj[:, :, w]
+        bar = 1e-6 * np.abs(ref_t[w]) + 1e-6
+        assert np.all(np.abs(ours - ref_t[w]) <= bar), (w, float(np.max(np.abs(ours - ref_t[w]) / bar)))
+        assert np.all(np.abs(ours - ref_d[w]) <= np.abs(ref_d[w] - ref_t[w]) + bar), w
+    chi_t, chi_d = fx[f"{group}/tight/chi"], fx[f"{group}/default/chi"]
+    rel = np.abs(chi / chi_t - 1)
+    assert np.all(rel <= 1e-6), rel
+    assert np.all(rel <= 2 * np.abs(chi_d / chi_t - 1) + 1e-7), (rel, np.abs(chi_d / chi_t - 1))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ours_ok = np.isfinite(np.log(_preds(golden, traj)))
+        ref_ok = np.isfinite(np.log(fx[f"{group}/default/pred"]))
+    assert np.array_equal(ours_ok, ref_ok)
+    if group == "stiff" and method == "auto":
+        assert (st & 8).all(), st               # every stiff draw handed to BDF

@@ -213,3 +213,35 @@ def test_bench_two_ranks_rehearsal():
     assert c4["walkers_total"] == 1 << 20 and c4["walkers_per_gpu"] == 1 << 19 and c4["n_gpus"] == 2
     assert c4["allgather"]["bytes_gathered"] == 49 * 10 * (1 << 20) * 8
     assert c4["integrate"]["chi_finite"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("counts", [[5, 3], [4, 4, 1], [7, 0, 7, 6, 7, 7, 2, 7], [131072, 131071]])
+def test_pool_pad_and_relayout_n_ranks_on_one_gpu(counts):
+    """The data movement oe_allgather_samples does around the RCCL collective for n > 1 ranks
+    (comm.hip: pad each rank's [rows][count] block to [rows][cmax]; lay the rank-major
+    [n][rows][cmax] result out as [rows][sum(counts)] in global walker order), driven through
+    the C-ABI on one GPU with a synthetic gathered buffer — the path an 8-GPU pooling takes,
+    checked against a numpy re-layout for n = 2, 3, 8, ragged counts (one rank empty) and the
+    C4 shard size."""
+    import numpy as np
+    import torch
+    from odelib_amd import _native as N
+    dev = torch.device("cuda", 0)
+    n, rows = len(counts), 7
+    cmax = max(counts)
+    rs = np.random.RandomState(len(counts))
+    blocks = [rs.standard_normal((rows, c)) for c in counts]
+    # each rank pads its block (oe_pool_pad) into its slot of the rank-major buffer, as the
+    # collective would deliver it
+    gathered = torch.full((n, rows, cmax), np.nan, dtype=torch.float64, device=dev)
+    for r, b in enumerate(blocks):
+        tb = torch.as_tensor(b, device=dev).contiguous()
+        N.pool_pad(rows, tb.data_ptr() if b.size else None, counts[r], cmax, gathered[r].data_ptr())
+    g = gathered.cpu().numpy()
+    for r, b in enumerate(blocks):
+        assert np.array_equal(g[r, :, :counts[r]], b) and not g[r, :, counts[r]:].any()
+    out = torch.full((rows, sum(counts)), np.nan, dtype=torch.float64, device=dev)
+    N.pool_relayout(counts, rows, gathered.data_ptr(), out.data_ptr())
+    want = np.concatenate(blocks, axis=1)
+    assert np.array_equal(out.cpu().numpy(), want)

@@ -101,3 +101,33 @@ def test_masked_chi_semantics():
     # an all-masked proposal is never accepted (acc > u is masked -> falsy)
     acc = np.exp(0.0 - cpu_ref.chi(O, np.full(4, np.nan), np.ones(4)))
     assert not bool(acc > 0.5)
+
+
+def _stiff_fixture():
+    import os
+
+    from helpers import GOLDEN
+    return dict(np.load(os.path.join(GOLDEN, "stiff.npz")))
+
+
+@pytest.mark.parametrize("group", ["near", "stiff"])
+@pytest.mark.parametrize("tag,tol", [("default", None), ("tight", 1e-13)])
+def test_stiff_and_near_posterior_fixtures_bit_exact(group, tag, tol):
+    """tests/golden/stiff.npz (make_golden_stiff.py: the reference's integrate + get_chi at
+    odeint's default tolerance and at rtol = atol = 1e-13, on 16 near-posterior walkers and
+    on stiff draws where LSODA runs BDF): the oracle's odeint call and masked chi reproduce
+    them bit for bit."""
+    fx = _stiff_fixture()
+    m = oracle_model("two_i")
+    y0 = [m.istates[s] for s in CONFIGS["two_i"]["snames"]]
+    TH = fx[f"{group}/theta"]
+    for w in range(TH.shape[0]):
+        traj = cpu_ref.odeint_traj(CONFIGS["two_i"]["ode"], y0, m.times, TH[w], rtol=tol, atol=tol)
+        assert np.array_equal(traj, fx[f"{group}/{tag}/traj"][w]), w
+        for p, v in zip(m._pnames, TH[w]):
+            m.parameters[p].val = np.array(v)
+        m.integrator = (lambda yy, ps, tr=traj: tr)
+        d = m.integrate_obs()
+        assert np.array_equal(np.concatenate([d[s] for s in d]), fx[f"{group}/{tag}/pred"][w])
+        assert float(m.get_chi(d)) == fx[f"{group}/{tag}/chi"][w]
+        assert float(m.get_Rsqrd(d)) == fx[f"{group}/{tag}/rsq"][w]
