@@ -229,12 +229,21 @@ __device__ __forceinline__ void bdf_factor(BdfState<M::S>& st, double c, const d
   st.any_swap = ros::lu_factor<S>(st.lu, st.piv, st.dinv);
 }
 
+// What an accepted step hands to the (order-generic) output and order selection.
+struct BdfAccepted {
+  double h, en, safety;  // the step size used, the wave error norm, the Newton-count safety
+  double em_l, ep_l;     // this lane's norms at orders q − 1 and q + 1 (select steps)
+  bool select;           // wave-uniform: order and step selection after this step
+};
+
 // One step attempt at order Q (compile-time, so the difference rows are fixed registers and
-// the loops over them are straight-line code).
-template <class M, int PMAX, bool TRAJ, bool NT, int Q>
-__device__ __forceinline__ void bdf_step(const DevProblem& pb, BdfState<M::S>& st, double (&y)[M::S],
-                                         const double (&p)[PMAX], double* traj, int64_t W, int64_t w, bool active,
-                                         Acc& a) {
+// the loops over them are straight-line code).  Returns false on a rejected attempt (h and D
+// already rescaled for the retry); on acceptance the lanes' differences are updated and the
+// grid output and order selection follow in bdf_output / bdf_select (order-generic: written
+// once rather than once per order).
+template <class M, int PMAX, int Q>
+__device__ __forceinline__ bool bdf_attempt(const DevProblem& pb, BdfState<M::S>& st, const double (&p)[PMAX],
+                                            BdfAccepted& acc) {
   using namespace bdf;
   constexpr int S = M::S;
   const double rtol = pb.rtol, atol = pb.atol, ntol = pb.newton_tol;
@@ -320,7 +329,7 @@ __device__ __forceinline__ void bdf_step(const DevProblem& pb, BdfState<M::S>& s
     change_D<S>(st.D, Q, 0.5);
     st.neq = 0;
     st.lu_ok = false;
-    return;
+    return false;
   }
   const double safety = kconst(kSafety)[niter];
   const cptr<double> ec = kconst(kEc);
@@ -331,19 +340,20 @@ __device__ __forceinline__ void bdf_step(const DevProblem& pb, BdfState<M::S>& s
     st.h = h * factor;
     change_D<S>(st.D, Q, factor);
     st.neq = 0;
-    return;
+    return false;
   }
-  // accepted: differences, this lane's grid points, lanes that reach t_end leave
 #ifdef OE_BDF_TRACE
   if (st.live && blockIdx.x == 0 && threadIdx.x == 0) printf("ACC Q=%d t=%.17g h=%.17g niter=%d\n", Q, st.t, h, niter);
 #endif
   ++st.neq;
   st.fresh = false;
-  const bool select = st.neq >= Q + 1;  // wave-uniform: order and step selection after this step
-  double em_l = 0.0, ep_l = 0.0;
-  bool voter = false;
-  if (st.live) {
-    const double tn = st.t + h;
+  acc.h = h;
+  acc.en = en;
+  acc.safety = safety;
+  acc.select = st.neq >= Q + 1;
+  acc.em_l = 0.0;
+  acc.ep_l = 0.0;
+  if (st.live) {  // the differences of the accepted step
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       st.D[Q + 2][s] = d[s] - st.D[Q + 1][s];
@@ -353,59 +363,81 @@ __device__ __forceinline__ void bdf_step(const DevProblem& pb, BdfState<M::S>& s
     for (int j = Q; j >= 0; --j)
 #pragma unroll
       for (int s = 0; s < S; ++s) st.D[j][s] = st.D[j][s] + st.D[j + 1][s];
-    ++st.nst;
-    double yo[S];
-    const double* times = pb.times;
-    double rden[Q + 1];  // 1/(j·h): one division per order per step, not per grid point
+    if (acc.select) {  // the candidates' norms (used by the lanes still running after the output)
+      if constexpr (Q > 1) acc.em_l = norm_max<S>(ec[Q - 1], st.D[Q], yn, rtol, atol);
+      if constexpr (Q < kMaxQ) acc.ep_l = norm_max<S>(ec[Q + 1], st.D[Q + 2], yn, rtol, atol);
+    }
+  }
+  return true;
+}
+
+// The grid points of an accepted step of order q (wave-uniform, runtime) from the
+// backward-difference interpolant; a lane past its last grid point leaves (y = that row).
+template <int S, bool TRAJ, bool NT>
+__device__ __forceinline__ void bdf_output(const DevProblem& pb, BdfState<S>& st, int q, double h, double (&y)[S],
+                                           double* traj, int64_t W, int64_t w, bool active, Acc& a) {
+  using namespace bdf;
+  if (!st.live) return;
+  const double tn = st.t + h;
+  ++st.nst;
+  double yo[S];
+  const double* times = pb.times;
+  double rden[kMaxQ + 1];  // 1/(j·h): one division per order per step, not per grid point
 #pragma unroll
-    for (int j = 1; j <= Q; ++j) rden[j] = 1.0 / ((double)j * h);
-    while (st.i < pb.T && times[st.i] <= tn) {
-      const double ti = times[st.i];
-      double prod = 1.0;
+  for (int j = 1; j <= kMaxQ; ++j) {
+    if (j > q) break;
+    rden[j] = 1.0 / ((double)j * h);
+  }
+  while (st.i < pb.T && times[st.i] <= tn) {
+    const double ti = times[st.i];
+    double prod = 1.0;
 #pragma unroll
-      for (int s = 0; s < S; ++s) yo[s] = st.D[0][s];
+    for (int s = 0; s < S; ++s) yo[s] = st.D[0][s];
 #pragma unroll
-      for (int j = 1; j <= Q; ++j) {
-        const double x = (ti - (tn - (double)(j - 1) * h)) * rden[j];
-        prod = prod * x;
+    for (int j = 1; j <= kMaxQ; ++j) {
+      if (j > q) break;
+      const double x = (ti - (tn - (double)(j - 1) * h)) * rden[j];
+      prod = prod * x;
 #pragma unroll
-        for (int s = 0; s < S; ++s) yo[s] = fma(st.D[j][s], prod, yo[s]);
-      }
+      for (int s = 0; s < S; ++s) yo[s] = fma(st.D[j][s], prod, yo[s]);
+    }
 #ifdef OE_BDF_TRACE
-      if (blockIdx.x == 0 && threadIdx.x == 0) printf("EMIT i=%d y1=%.17g\n", st.i, yo[1]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) printf("EMIT i=%d y1=%.17g\n", st.i, yo[1]);
 #endif
-      emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, a);
-      ++st.i;
-      st.nst = 0;
-    }
-    st.t = tn;
-    if (st.i >= pb.T) {
+    emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, a);
+    ++st.i;
+    st.nst = 0;
+  }
+  st.t = tn;
+  if (st.i >= pb.T) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) y[s] = yo[s];
-      st.live = false;
-    } else if (select) {
-      voter = true;
-      if constexpr (Q > 1) em_l = norm_max<S>(ec[Q - 1], st.D[Q], yn, rtol, atol);
-      if constexpr (Q < kMaxQ) ep_l = norm_max<S>(ec[Q + 1], st.D[Q + 2], yn, rtol, atol);
-    }
+    for (int s = 0; s < S; ++s) y[s] = yo[s];
+    st.live = false;
   }
-  if (select && __ballot(voter) != 0ull) {
-    const double em = wave_max(em_l), ep = wave_max(ep_l);
-    const double fm = (Q > 1) ? inv_root(em, Q) : 0.0;
-    const double fe = inv_root(en, Q + 1);
-    const double fp = (Q < kMaxQ) ? inv_root(ep, Q + 2) : 0.0;
-    int dq = 0;
-    double fmx = fm;
-    if (fe > fmx) { fmx = fe; dq = 1; }
-    if (fp > fmx) { fmx = fp; dq = 2; }
-    const int q = Q + dq - 1;
-    const double factor = fmin(10.0, safety * fmx);
-    st.h = h * factor;
-    change_D<S>(st.D, q, factor);
-    st.order = q;
-    st.neq = 0;
-    st.lu_ok = false;
-  }
+}
+
+// Order and step-size selection after an accepted select step of order q (scipy's rule:
+// the largest of the three factors, capped at 10), voted by the lanes still running.
+template <int S>
+__device__ __forceinline__ void bdf_select(BdfState<S>& st, int q, const BdfAccepted& acc) {
+  using namespace bdf;
+  const bool voter = st.live;
+  if (__ballot(voter) == 0ull) return;
+  const double em = wave_max(voter ? acc.em_l : 0.0), ep = wave_max(voter ? acc.ep_l : 0.0);
+  const double fm = (q > 1) ? inv_root(em, q) : 0.0;
+  const double fe = inv_root(acc.en, q + 1);
+  const double fp = (q < kMaxQ) ? inv_root(ep, q + 2) : 0.0;
+  int dq = 0;
+  double fmx = fm;
+  if (fe > fmx) { fmx = fe; dq = 1; }
+  if (fp > fmx) { fmx = fp; dq = 2; }
+  const int nq = q + dq - 1;
+  const double factor = fmin(10.0, acc.safety * fmx);
+  st.h = acc.h * factor;
+  change_D<S>(st.D, nq, factor);
+  st.order = nq;
+  st.neq = 0;
+  st.lu_ok = false;
 }
 
 // BDF integration of the lanes with `part` set from their own (t, y, grid index i,
@@ -472,12 +504,19 @@ __device__ __forceinline__ void integrate_bdf(const DevProblem& pb, double (&y)[
   st.fresh = false;
   st.any_swap = false;
   while (__ballot(st.live) != 0ull) {
-    switch (st.order) {  // wave-uniform
-      case 1: bdf_step<M, PMAX, TRAJ, NT, 1>(pb, st, y, p, traj, W, w, active, a); break;
-      case 2: bdf_step<M, PMAX, TRAJ, NT, 2>(pb, st, y, p, traj, W, w, active, a); break;
-      case 3: bdf_step<M, PMAX, TRAJ, NT, 3>(pb, st, y, p, traj, W, w, active, a); break;
-      case 4: bdf_step<M, PMAX, TRAJ, NT, 4>(pb, st, y, p, traj, W, w, active, a); break;
-      default: bdf_step<M, PMAX, TRAJ, NT, 5>(pb, st, y, p, traj, W, w, active, a); break;
+    const int q = st.order;  // wave-uniform
+    BdfAccepted acc;
+    bool ok;
+    switch (q) {
+      case 1: ok = bdf_attempt<M, PMAX, 1>(pb, st, p, acc); break;
+      case 2: ok = bdf_attempt<M, PMAX, 2>(pb, st, p, acc); break;
+      case 3: ok = bdf_attempt<M, PMAX, 3>(pb, st, p, acc); break;
+      case 4: ok = bdf_attempt<M, PMAX, 4>(pb, st, p, acc); break;
+      default: ok = bdf_attempt<M, PMAX, 5>(pb, st, p, acc); break;
+    }
+    if (ok) {
+      bdf_output<S, TRAJ, NT>(pb, st, q, acc.h, y, traj, W, w, active, a);
+      if (acc.select) bdf_select<S>(st, q, acc);
     }
     // budget: a lane that needs more than `budget` steps inside one output interval, or a
     // step below hmin, is abandoned (MAXSTEP, NaN for the rest of its grid)

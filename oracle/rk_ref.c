@@ -1150,6 +1150,14 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
           ++b->nst;
           double yo[MAXS], rden[BDF_MAXQ + 1];
           for (int j = 1; j <= order; ++j) rden[j] = 1.0 / ((double)j * h);
+          if (getenv("RKREF_BDF_TRACE_D") && l == 0) {
+            fprintf(stderr, "STEPD q=%d tn=%a h=%a i=%d\n", order, tn, h, b->i);
+            for (int j = 0; j <= order; ++j) {
+              fprintf(stderr, "STEPD D%d", j);
+              for (int s = 0; s < S; ++s) fprintf(stderr, " %a", b->D[j][s]);
+              fprintf(stderr, "\n");
+            }
+          }
           while (b->i < pb->T && pb->times[b->i] <= tn) {
             const double ti = pb->times[b->i];
             double prod = 1.0;
@@ -1159,7 +1167,17 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
               prod = prod * x;
               for (int s = 0; s < S; ++s) yo[s] = fma(b->D[j][s], prod, yo[s]);
             }
-            if (getenv("RKREF_BDF_TRACE") && l == 0) fprintf(stderr, "EMIT i=%d y1=%.17g\n", b->i, yo[1]);
+            if (getenv("RKREF_BDF_TRACE") && l == 0) {
+              fprintf(stderr, "EMIT i=%d y1=%.17g\n", b->i, yo[1]);
+              if (getenv("RKREF_BDF_TRACE_D")) {
+                fprintf(stderr, "EMITD q=%d ti=%a tn=%a h=%a t=%a\n", order, ti, tn, h, b->t);
+                for (int j = 0; j <= order + 2; ++j) {
+                  fprintf(stderr, "EMITD D%d", j);
+                  for (int s = 0; s < S; ++s) fprintf(stderr, " %a", b->D[j][s]);
+                  fprintf(stderr, "\n");
+                }
+              }
+            }
             if (needs_emit(pb, tr, b->i, q->kobs)) emit(pb, b->i, yo, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
             ++b->i;
             b->nst = 0;
