@@ -69,7 +69,7 @@ def parse():
                     help="continue the untimed warm-up until this much wall time has passed")
     ap.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
     ap.add_argument("--model", default="two_i", help="two_i | chain<N>")
-    ap.add_argument("--method", default="rk4", choices=["rk4", "dopri5"])
+    ap.add_argument("--method", default="rk4", choices=["rk4", "dopri5", "auto", "bdf", "rosenbrock"])
     ap.add_argument("--times", type=int, default=1000)
     ap.add_argument("--cached-stores", action="store_true", help="plain (cached) trajectory stores")
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "half", "pipe2", "pipe4", "pipe8", "pipe2x", "pipe4x", "pipe8x"],
@@ -724,6 +724,10 @@ def extra_configs(args, R, T, P):
     # 20-state RK4 tolerance; tests/test_gpu_parity.py::test_c3_rk4_bench_accuracy);
     # rk4_substeps=3 is within rtol = atol = 1e-6 (2 is not: 1.09 of that budget).
     cfgs = (("C2", "two_i", "dopri5", 65536, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"),
+            # C2 on the store-wave kernel (4 compute + 4 store waves per workgroup, per-wave LDS
+            # slot rings with produced/consumed counters, no phase barrier; bitwise the direct
+            # kernel: tests/test_gpu_dopri5_piped.py)
+            ("C2-storewaves", "two_i", "dopri5", 65536, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"),
             ("C2-auto", "two_i", "auto", 65536, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"),
             ("C2-stiffmix-dopri5", "two_i", "dopri5", 65536, 1e-3, 1, "rtol=atol=1.49012e-8"),
             ("C2-stiffmix-auto", "two_i", "auto", 65536, 1e-3, 1, "rtol=atol=1.49012e-8"),
@@ -734,7 +738,8 @@ def extra_configs(args, R, T, P):
             ("C3-dopri5-onelane", "chain20", "dopri5", 262144, 0.0, 1, "rtol=atol=1.49012e-8 (odeint defaults)"))
     for name, model, method, W, stiff, subs, tol in cfgs:
         split = not name.endswith("-onelane")
-        kern = ("half" if args.half_waves else args.kernel) if method == "rk4" else None
+        kern = (("half" if args.half_waves else args.kernel) if method == "rk4"
+                else "pipe2" if name.endswith("-storewaves") else None)
         ex, y0x = R.engine(model, method, T, subs)
         Sx = len(y0x)
         thh = synthetic_walkers(W, P)
@@ -769,6 +774,8 @@ def extra_configs(args, R, T, P):
         if method == "rk4":
             extra[name]["rk4_substeps"] = subs
             extra[name]["kernel"] = ex.last_variant()
+        if name.endswith("-storewaves"):
+            extra[name]["kernel"] = "k_integrate_dopri5_piped (OE_PIPE)"
         if model == "chain20" and method == "dopri5":
             extra[name]["lanes_per_walker"] = 2 if split else 1
         if n_stiff:

@@ -158,27 +158,12 @@ __device__ __forceinline__ void row(const double (&D)[kRows][S], int j, double (
 }
 }  // namespace bdf
 
-// Output of one lane at its own grid index i (trajectory row store + minimum + observations):
-// per-lane addresses, so plain stores/loads instead of the uniform buffer descriptors.
-// Without a trajectory only observed grid points are emitted (as the DOPRI5 pass does).
-template <int S, bool TRAJ, bool NT>
-__device__ __forceinline__ void emit_lane(const DevProblem& pb, int i, const double (&y)[S], double* traj, int64_t W,
-                                          int64_t w, bool active, int& k, Acc& a) {
+// the observations at grid index i (the lane's next observed one): fused chi / R² terms, and
+// the next observed index
+template <int S>
+__device__ __forceinline__ void observe_lane(const DevProblem& pb, int i, const double (&y)[S], int& k, int& nxt,
+                                             Acc& a) {
   const Obs* obs = pb.obs;
-  const bool observed = k < pb.n_obs && obs[k].tidx == i;
-  if (!TRAJ && !observed) return;
-  track_min<S>(y, a);
-  if constexpr (TRAJ) {
-    if (active) {
-      double* row = traj + (int64_t)i * S * W + w;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if constexpr (NT) __builtin_nontemporal_store(y[s], row + (int64_t)s * W);
-        else row[(int64_t)s * W] = y[s];
-      }
-    }
-  }
-  if (!observed) return;
   check_finite(y, a);
   while (k < pb.n_obs && obs[k].tidx == i) {
     const uint64_t mask = obs[k].mask;
@@ -195,6 +180,33 @@ __device__ __forceinline__ void emit_lane(const DevProblem& pb, int i, const dou
     if (!__builtin_isnan(r2)) a.ssres += r2;
     ++k;
   }
+  nxt = (k < pb.n_obs) ? obs[k].tidx : 0x7fffffff;
+}
+
+// Output of one lane at its own grid index i (trajectory row store + minimum + observations):
+// per-lane addresses, so plain stores/loads instead of the uniform buffer descriptors.
+// Without a trajectory only observed grid points are emitted (as the DOPRI5 pass does).
+// `nxt` is the lane's next observed grid index, carried in a register: an unobserved row does
+// no load.  The row stores come last: on gfx950 a vector load's wait also waits for every
+// store issued before it, so a load after the stores (the old obs[k] test) held each row
+// until its stores had completed (C2-stiffmix `auto`: ~2.3 us per BDF row).
+template <int S, bool TRAJ, bool NT>
+__device__ __forceinline__ void emit_lane(const DevProblem& pb, int i, const double (&y)[S], double* traj, int64_t W,
+                                          int64_t w, bool active, int& k, int& nxt, Acc& a) {
+  const bool observed = i == nxt;
+  if (!TRAJ && !observed) return;
+  track_min<S>(y, a);
+  if (observed) observe_lane<S>(pb, i, y, k, nxt, a);
+  if constexpr (TRAJ) {
+    if (active) {
+      double* row = traj + (int64_t)i * S * W + w;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if constexpr (NT) __builtin_nontemporal_store(y[s], row + (int64_t)s * W);
+        else row[(int64_t)s * W] = y[s];
+      }
+    }
+  }
 }
 
 // The per-lane state of the BDF pass and the wave-shared controls.
@@ -204,7 +216,9 @@ struct BdfState {
   double lu[S][S], dinv[S]; // LU of I − c·J (J evaluated when the factors are built)
   int piv[S];
   double t;                 // this lane's time
+  double ti;                // times[i] (times[T] is the +inf sentinel), loaded ahead
   int i, k, nst;            // next grid index, next observation, steps since the last grid point
+  int nxt;                  // grid index of observation k (INT_MAX past the last)
   bool live;
   // wave-uniform
   double h;
@@ -388,24 +402,29 @@ __device__ __forceinline__ void bdf_output(const DevProblem& pb, BdfState<S>& st
     if (j > q) break;
     rden[j] = 1.0 / ((double)j * h);
   }
-  while (st.i < pb.T && times[st.i] <= tn) {
-    const double ti = times[st.i];
-    double prod = 1.0;
+  while (st.ti <= tn) {  // (st.i < T: times[T] is +inf)
+    const double ti = st.ti;
+    const int i = st.i;
+    st.i = i + 1;
+    const double tnext = times[st.i];  // in flight while this row is formed and stored
+    if (TRAJ || i == st.nxt || i == pb.T - 1) {  // without a trajectory: observed rows, the final state
+      double prod = 1.0;
 #pragma unroll
-    for (int s = 0; s < S; ++s) yo[s] = st.D[0][s];
+      for (int s = 0; s < S; ++s) yo[s] = st.D[0][s];
 #pragma unroll
-    for (int j = 1; j <= kMaxQ; ++j) {
-      if (j > q) break;
-      const double x = (ti - (tn - (double)(j - 1) * h)) * rden[j];
-      prod = prod * x;
+      for (int j = 1; j <= kMaxQ; ++j) {
+        if (j > q) break;
+        const double x = (ti - (tn - (double)(j - 1) * h)) * rden[j];
+        prod = prod * x;
 #pragma unroll
-      for (int s = 0; s < S; ++s) yo[s] = fma(st.D[j][s], prod, yo[s]);
-    }
+        for (int s = 0; s < S; ++s) yo[s] = fma(st.D[j][s], prod, yo[s]);
+      }
 #ifdef OE_BDF_TRACE
-    if (blockIdx.x == 0 && threadIdx.x == 0) printf("EMIT i=%d y1=%.17g\n", st.i, yo[1]);
+      if (blockIdx.x == 0 && threadIdx.x == 0) printf("EMIT i=%d y1=%.17g\n", i, yo[1]);
 #endif
-    emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, a);
-    ++st.i;
+      emit_lane<S, TRAJ, NT>(pb, i, yo, traj, W, w, active, st.k, st.nxt, a);
+    }
+    st.ti = tnext;
     st.nst = 0;
   }
   st.t = tn;
@@ -458,6 +477,8 @@ __device__ __forceinline__ void integrate_bdf(const DevProblem& pb, double (&y)[
   st.t = t;
   st.i = i;
   st.k = k;
+  st.ti = pb.times[i];
+  st.nxt = (k < pb.n_obs) ? pb.obs[k].tidx : 0x7fffffff;
   st.nst = 0;
   {
     double f[S];
@@ -526,7 +547,7 @@ __device__ __forceinline__ void integrate_bdf(const DevProblem& pb, double (&y)[
       double yo[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
-      for (; st.i < pb.T; ++st.i) emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, a);
+      for (; st.i < pb.T; ++st.i) emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, st.nxt, a);
 #pragma unroll
       for (int s = 0; s < S; ++s) y[s] = yo[s];
     }
