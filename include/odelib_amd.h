@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define OE_ABI_VERSION 5
+#define OE_ABI_VERSION 6
 
 /* return codes */
 enum {

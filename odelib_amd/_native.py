@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ODELIB_AMD_LIB", os.path.join(_HERE, "csrc", "libodelib_amd.so"))
 
 # --- constants mirrored from include/odelib_amd.h -----------------------------------
-OE_ABI_VERSION = 5
+OE_ABI_VERSION = 6
 OE_COMM_ID_BYTES = 128
 OE_OK = 0
 OE_ERR_ARG, OE_ERR_HIP, OE_ERR_STATE, OE_ERR_UNSUPPORTED, OE_ERR_NOMEM = -1, -2, -3, -4, -5
