@@ -764,10 +764,11 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
   if (c->d_rk4) { OE_HIP(c, hipFree(c->d_rk4)); c->d_rk4 = nullptr; }
   OE_HIP(c, hipMalloc(&c->d_rk4, sizeof(double) * rk4.size()));
   OE_HIP(c, hipMemcpy(c->d_rk4, rk4.data(), sizeof(double) * rk4.size(), hipMemcpyHostToDevice));
-  // the grid plus a +inf sentinel at index T: the DOPRI5 dense-output loop reads the
-  // next grid time one point ahead without clamping the index
+  // the grid plus +inf sentinels from index T: the DOPRI5 dense-output loop reads the
+  // next grid time one point ahead, the per-lane DOPRI5 (lane.cuh) a window of kGridWin,
+  // without clamping the index
   std::vector<double> tg(p->times, p->times + p->n_times);
-  tg.push_back(HUGE_VAL);
+  tg.insert(tg.end(), oe::kGridWin + 1, HUGE_VAL);
   OE_HIP(c, hipMalloc(&c->d_times, sizeof(double) * tg.size()));
   OE_HIP(c, hipMemcpy(c->d_times, tg.data(), sizeof(double) * tg.size(), hipMemcpyHostToDevice));
   if (p->n_obs > 0) {

@@ -936,18 +936,30 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
 }  // namespace oe
 #include "stiff.cuh"
 #include "bdf.cuh"
+#include "lane.cuh"
 namespace oe {
 
 // WAVE_REDO (batched integrate of models wider than kStiffRegS): 'auto' only marks the
 // walkers the DOPRI5 pass evicts (status ST_STIFF); k_stiff_wave redoes them one wave per
 // walker (stiff_wave.cuh).  The MH kernel redoes them in place (private-memory path).
-template <class M, int PMAX, int METHOD, bool TRAJ, bool NT, bool WAVE_REDO = false>
+// LANE (kernels without a trajectory, S <= 8): DOPRI5 with a step size per lane (lane.cuh)
+// instead of one per wave.
+#ifndef OE_LANE_INTEGRATE  // measurement / debug builds: chi-only oe_integrate on the per-lane DOPRI5 too
+#define OE_LANE_INTEGRATE 0
+#endif
+template <class M, int METHOD>
+constexpr bool kLaneSteps = (METHOD == kDOPRI5 || METHOD == kAuto) && M::S <= kStiffRegS;
+
+template <class M, int PMAX, int METHOD, bool TRAJ, bool NT, bool WAVE_REDO = false, bool LANE = false>
 __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, int64_t w, bool active, Acc& a) {
+  static_assert(!LANE || (!TRAJ && kLaneSteps<M, METHOD>), "per-lane steps: no trajectory, DOPRI5/auto, S <= 8");
   const uint32_t off = (uint32_t)w * 8u;  // byte offset of walker w in a [..][W] row
   if constexpr (METHOD == kRK4) {
     integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  } else if constexpr (LANE && METHOD == kDOPRI5) {
+    integrate_dopri5_lane<M, PMAX, false>(pb, y, p, W, off, active, a);
   } else if constexpr (METHOD == kDOPRI5 || M::S > kStiffMaxS) {
     integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
   } else if constexpr (METHOD == kBdf) {  // LSODA's BDF branch for every walker (S <= kStiffRegS)
@@ -955,6 +967,10 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
     int k = 0;
     emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
     integrate_bdf<M, PMAX, TRAJ, NT>(pb, y, kconst(pb.times)[0], 1, k, p, traj, W, w, active, active, a);
+  } else if constexpr (METHOD == kAuto && M::S <= kStiffRegS && LANE) {
+    // per-lane DOPRI5 whose flagged lanes continue with BDF from their own eviction points
+    // (the BDF pass is lane.cuh's tail: it starts from the DOPRI5 pass's live state)
+    integrate_dopri5_lane<M, PMAX, true>(pb, y, p, W, off, active, a);
   } else if constexpr (METHOD == kAuto && M::S <= kStiffRegS) {
     // LSODA-like: DOPRI5 with the stiffness test; a lane it evicts (stiff, or over the step
     // budget) continues from the eviction point with BDF (status bit ST_STIFF)
@@ -1073,7 +1089,8 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
   Acc a = acc_init();
-  integrate_walker<M, PMAX, METHOD, TRAJ, NT, (M::S > kStiffRegS)>(pb, y, p, ia.traj, W, w, active, a);
+  integrate_walker<M, PMAX, METHOD, TRAJ, NT, (M::S > kStiffRegS), (OE_LANE_INTEGRATE && !TRAJ && kLaneSteps<M, METHOD>)>(
+      pb, y, p, ia.traj, W, w, active, a);
   if (active) {
     if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
     if (ia.ssres) ia.ssres[w] = a.ssres;
@@ -1475,7 +1492,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int s = 0; s < S; ++s) y[s] = Row(y0g + (int64_t)s * W, W).ld(off);
     Acc a = acc_init();
-    integrate_walker<M, PMAX, METHOD, false, false>(pb, y, th, nullptr, W, w, active, a);
+    integrate_walker<M, PMAX, METHOD, false, false, false, kLaneSteps<M, METHOD>>(pb, y, th, nullptr, W, w, active, a);
     if (active) {
       const double chi = a.nvalid ? a.chi : __builtin_nan("");
       Row(ma.cur, W).st(off, chi);
@@ -1513,7 +1530,7 @@ __global__ void __launch_bounds__(256)
     }
     // ---- integrate + fused chi (Samplers.py:115-116)
     Acc a = acc_init();
-    integrate_walker<M, PMAX, METHOD, false, false>(pb, y, tn, nullptr, W, w, active, a);
+    integrate_walker<M, PMAX, METHOD, false, false, false, kLaneSteps<M, METHOD>>(pb, y, tn, nullptr, W, w, active, a);
     const double chin = a.nvalid ? a.chi : __builtin_nan("");
     theta = opaque(theta);
     y0g = opaque(y0g);
@@ -1656,7 +1673,7 @@ __global__ void __launch_bounds__(256)
     y[s] = (ma.any_walk && pi >= 0) ? pick(tn, pi) : Row(ma.y0 + (int64_t)s * W, W).ld(off);
   }
   Acc a = acc_init();
-  integrate_walker<M, PMAX, METHOD, false, false>(pb, y, tn, nullptr, ta.n_lanes, g, active, a);
+  integrate_walker<M, PMAX, METHOD, false, false, false, kLaneSteps<M, METHOD>>(pb, y, tn, nullptr, ta.n_lanes, g, active, a);
   if (active) {
     const int64_t NW = ta.n_lanes;
     const uint32_t o = (uint32_t)g * 8u;

@@ -60,6 +60,9 @@ typedef struct {
   int split;     /* DOPRI5 with a walker over `split` lanes (odelib_amd/csrc/split.cuh): groups of
                     64/split walkers share a step size; a walker's error norm is the argmax over
                     each lane's states, combined in a tree of lanes (lower lane kept on ties) */
+  int lane_steps; /* DOPRI5 / 'auto' without a trajectory, S <= 8 (odelib_amd/csrc/lane.cuh, the MH
+                     kernels): every walker takes its own step sizes, i.e. the lockstep algorithm
+                     on a group of one; the BDF pass of 'auto' stays one group of 64 */
 } Prob;
 
 static void rhs(const Prob* pb, const double* y, double t, const double* ps, double* dy) {
@@ -1241,7 +1244,10 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
 static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double* traj, int64_t W) {
   const int S = pb->S;
   if (S <= 8) {
-    dopri5_group(pb, L, nl, p, traj, W, 1);
+    if (pb->lane_steps)
+      for (int l = 0; l < nl; ++l) dopri5_group(pb, L + l, 1, p + l * MAXP, traj, W, 1);
+    else
+      dopri5_group(pb, L, nl, p, traj, W, 1);
     int any = 0;
     for (int l = 0; l < nl; ++l) {
       L[l].part = L[l].handed && L[l].active;
@@ -1276,7 +1282,7 @@ static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double*
 static Prob make_prob(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                       const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                       int substeps, double rtol, double atol, int max_steps) {
-  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol, 0, 0, 0};
+  Prob pb = {model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, max_steps, rtol, atol, 0, 0, 0, 0};
   pb.newton_tol = bdf_newton_tol(rtol);
   return pb;
 }
@@ -1317,7 +1323,10 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
     for (int l = 0; l < LANES; ++l)
       if (L[l].active) check_finite(pb->S, L[l].y, &L[l].a);
   } else if (pb->method == METHOD_DOPRI5) {
-    dopri5_group(pb, L, G, p, traj, W, 0);
+    if (pb->lane_steps)
+      for (int l = 0; l < G; ++l) dopri5_group(pb, L + l, 1, p + l * MAXP, traj, W, 0);
+    else
+      dopri5_group(pb, L, G, p, traj, W, 0);
   } else if (pb->method == METHOD_AUTO) {
     auto_group(pb, L, LANES, p, traj, W);
   } else if (pb->method == METHOD_BDF) {
@@ -1347,12 +1356,15 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
 int ref_integrate(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                   const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                   int substeps, double rtol, double atol, int max_steps, int64_t W, const double* y0,
-                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status, int split) {
+                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status, int split,
+                  int lane_steps) {
   if (S > MAXS || P > MAXP || W <= 0) return -1;
   if (split > 1 && (method != METHOD_DOPRI5 || split > 4 || S % split)) return -1;
+  if (lane_steps && (traj || split > 1 || S > 8 || (method != METHOD_DOPRI5 && method != METHOD_AUTO))) return -1;
   Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
   pb.wave_redo = S > 8; /* ode_kernels.cuh kStiffRegS */
   pb.split = split;
+  pb.lane_steps = lane_steps;
   const int G = group_size(&pb);
   const int64_t ngroups = (W + G - 1) / G;
   /* groups are independent: OpenMP over groups gives the same bits as the serial loop */
@@ -1423,6 +1435,8 @@ int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const
   if (split > 1 && (method != METHOD_DOPRI5 || split > 4 || S % split)) return -1;
   Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
   pb.split = split; /* the split MH kernel (split.cuh k_mh_split): 64/split walkers per step size */
+  /* the one-lane MH kernels step every chain on its own (ode_kernels.cuh kLaneSteps) */
+  pb.lane_steps = split <= 1 && S <= 8 && (method == METHOD_DOPRI5 || method == METHOD_AUTO);
   const int G = group_size(&pb);
   int any_walk = 0;
   for (int j = 0; j < P; ++j) any_walk |= walk[j] != 0;

@@ -28,7 +28,7 @@ def lib():
         vp, i32, i64, d, u64 = C.c_void_p, C.c_int, C.c_int64, C.c_double, C.c_uint64
         L.ref_integrate.restype = C.c_int
         L.ref_integrate.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, d, d, i32,
-                                    i64, vp, vp, vp, vp, vp, vp, i32]
+                                    i64, vp, vp, vp, vp, vp, vp, i32, i32]
         L.ref_mh.restype = C.c_int
         L.ref_mh.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, d, d, i32, d, i32,
                              i64, i64, i32, i32, i32, u64, d, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
@@ -99,10 +99,17 @@ def product_split(fp) -> int:
     return 1
 
 
-def integrate(fp, y0, theta, trajectory=True, split=None):
+def lane_steps(fp) -> bool:
+    """Whether the product's MH kernels step every chain on its own (ode_kernels.cuh
+    kLaneSteps, lane.cuh): DOPRI5 / 'auto', one lane per walker, at most 8 states."""
+    return fp.method in ("dopri5", "auto") and int(fp.n_states) <= 8 and product_split(fp) == 1
+
+
+def integrate(fp, y0, theta, trajectory=True, split=None, lane=False):
     """The engine's integrate restated.  ``split``: lanes per walker of the DOPRI5 kernel
     being checked (None: the product's choice for this problem, ``product_split``; 1: the
-    one-lane grouping, as the product's OE_NO_SPLIT)."""
+    one-lane grouping, as the product's OE_NO_SPLIT).  ``lane``: every walker with its own
+    DOPRI5 step sizes (the MH kernels' integrator, no trajectory; ``lane_steps``)."""
     pr = Problem(fp)
     split = product_split(fp) if split is None else int(split)
     y0 = np.ascontiguousarray(y0, dtype=np.float64)
@@ -113,7 +120,7 @@ def integrate(fp, y0, theta, trajectory=True, split=None):
     ssres = np.empty(W)
     status = np.empty(W, np.int32)
     rc = lib().ref_integrate(*pr.args(), W, _p(y0), _p(theta), _p(traj), _p(chi), _p(ssres), _p(status),
-                             split if split > 1 else 0)
+                             split if split > 1 else 0, int(bool(lane)))
     if rc:
         raise RuntimeError("ref_integrate failed")
     return {"traj": traj, "chi": chi, "ssres": ssres, "status": status}
@@ -219,7 +226,8 @@ def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3
     walk = np.asarray(walk_mask, bool)
     ip = np.full(S, -1) if init_param is None else np.asarray(init_param)
     any_walk = walk.any()
-    a0 = integrate(fp, y0, theta, trajectory=False, split=split)
+    lane = lane_steps(fp) and split == 1
+    a0 = integrate(fp, y0, theta, trajectory=False, split=split, lane=lane)
     chi = a0["chi"].copy()
     rsq = 1.0 - a0["ssres"] / pr.sstot
     aic = -2.0 * (-chi) + 2.0 * pr.pnum
@@ -260,7 +268,7 @@ def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3
                         ys[:, s] = tn[:, ip[s]]
             res = integrate(fp, np.ascontiguousarray(ys.transpose(1, 0, 2).reshape(S, N * W)),
                             np.ascontiguousarray(tn.transpose(1, 0, 2).reshape(P, N * W)), trajectory=False,
-                            split=split)
+                            split=split, lane=lane)
             nchi = res["chi"].reshape(N, W)
             nss = res["ssres"].reshape(N, W)
             nst = res["status"].reshape(N, W)

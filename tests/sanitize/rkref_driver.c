@@ -13,7 +13,8 @@
 int ref_integrate(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx,
                   const uint64_t* mask, const double* O, const double* two_s2, const double* lin, int method,
                   int substeps, double rtol, double atol, int max_steps, int64_t W, const double* y0,
-                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status, int split);
+                  const double* theta, double* traj, double* chi, double* ssres, int32_t* status, int split,
+                  int lane_steps);
 int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const int32_t* tidx, const uint64_t* mask,
            const double* O, const double* two_s2, const double* lin, int method, int substeps, double rtol,
            double atol, int max_steps, double sstot, int pnum, int64_t W, int64_t walker_offset, int nits, int burnin,
@@ -55,7 +56,9 @@ static void run_case(int model, int S, int P, int64_t W, int method, int with_tr
   double* ss = malloc(sizeof(double) * W);
   int32_t* st = malloc(sizeof(int32_t) * W);
   int rc = ref_integrate(model, S, P, T, times, NOBS, tidx, mask, O, two_s2, lin, method, 2, 1.49012e-8, 1.49012e-8,
-                         60, W, y0, th, traj, chi, ss, st, split);
+                         60, W, y0, th, traj, chi, ss, st, split,
+                         /* without a trajectory: the MH kernels' per-lane DOPRI5 (lane.cuh) */
+                         !with_traj && split <= 1 && S <= 8 && (method == 1 || method == 2));
   if (rc) { fprintf(stderr, "ref_integrate rc=%d (model %d S %d method %d)\n", rc, model, S, method); exit(1); }
   /* Metropolis-Hastings: Philox, then replay with a linked initial state (P + 1) */
   const int nits = 9, burnin = 3, kept = nits - 1 - burnin;
