@@ -35,7 +35,13 @@ constexpr int kGridWin = 8;  // the time grid buffer carries kGridWin + 1 +inf s
 
 // AUTO (S <= kStiffRegS): the stiffness test of integrate_dopri5 hands the lane over at
 // its eviction point, as does the step budget; the BDF pass at the end continues it from
-// the loop's live state (t, y, grid index, observation index, accumulators).
+// the loop's live state (t, y, grid index, observation index, accumulators).  (With that
+// state copied into a Resume struct and the BDF pass run by the caller, as the lockstep
+// path does, the MH kernels — 400+ SGPRs spilled to VGPR lanes — returned garbage from the
+// BDF pass for the handed lanes, and any printf or extra store around the call made it
+// right again: a code-generation fragility, not an algorithm difference.  This shape is
+// bitwise the C restatement in every kernel: tests/test_gpu_stiff.py,
+// test_gpu_speculative.py.)
 template <class M, int PMAX, bool AUTO>
 __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, double (&y)[M::S],
                                                       const double (&p)[PMAX], int64_t W, uint32_t off,
