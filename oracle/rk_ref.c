@@ -971,6 +971,15 @@ static void bdf_factor(const Prob* pb, BdfLane* b, double c, const double* y, do
 }
 
 static long long g_bdf_stats[3]; /* steps (accepted + rejected), Jacobians, groups */
+/* per-phase counts (tools: where a BDF step's time goes): accepted, rejected on the error,
+   rejected on Newton, Newton iterations, order/step selections, grid points emitted */
+static long long g_bdf_detail[6];
+void ref_bdf_detail(long long* out, int reset) {
+  for (int j = 0; j < 6; ++j) {
+    out[j] = g_bdf_detail[j];
+    if (reset) g_bdf_detail[j] = 0;
+  }
+}
 void ref_bdf_stats(long long* out, int reset) {
   for (int j = 0; j < 3; ++j) {
     out[j] = g_bdf_stats[j];
@@ -1107,6 +1116,8 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
       }
       bad = 0;
       for (int l = 0; l < nl; ++l) bad |= B[l].live && !B[l].conv;
+#pragma omp atomic
+      g_bdf_detail[3] += niter;
       if (!bad || fresh) break;
       for (int l = 0; l < nl; ++l)
         if (B[l].live) bdf_factor(pb, &B[l], c, B[l].yp, B[l].t + h, p + l * MAXP);
@@ -1114,6 +1125,8 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
       fresh = 1;
     }
     if (bad) {
+#pragma omp atomic
+      g_bdf_detail[2] += 1;
       h = h * 0.5;
       bdf_change_D(B, nl, order, 0.5, S);
       neq = 0;
@@ -1128,6 +1141,8 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
         en = fmax(en, b->el);
       }
       if (en > 1.0) {
+#pragma omp atomic
+        g_bdf_detail[1] += 1;
         const double factor = fmax(0.2, safety * inv_root(en, order + 1));
         h = h * factor;
         bdf_change_D(B, nl, order, factor, S);
@@ -1137,6 +1152,8 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
         if (getenv("RKREF_BDF_TRACE") && B[0].live) fprintf(stderr, "ACC Q=%d t=%.17g h=%.17g niter=%d\n", order, B[0].t, h, niter);
         ++neq;
         fresh = 0;
+#pragma omp atomic
+        g_bdf_detail[0] += 1;
         double em = 0.0, ep = 0.0;
         int voters = 0;
         for (int l = 0; l < nl; ++l) {
@@ -1182,6 +1199,8 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
               }
             }
             if (needs_emit(pb, tr, b->i, q->kobs)) emit(pb, b->i, yo, q->active ? traj : NULL, W, q->w, &q->kobs, &q->a);
+#pragma omp atomic
+            g_bdf_detail[5] += 1;
             ++b->i;
             b->nst = 0;
           }
@@ -1192,6 +1211,10 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
             continue;
           }
           if (neq >= order + 1) {
+            if (l == 0) {
+#pragma omp atomic
+              g_bdf_detail[4] += 1;
+            }
             ++voters;
             if (order > 1) em = fmax(em, bdf_norm(S, bdf_ec[order - 1], b->D[order], b->yn, rtol, atol));
             if (order < BDF_MAXQ) ep = fmax(ep, bdf_norm(S, bdf_ec[order + 1], b->D[order + 2], b->yn, rtol, atol));

@@ -174,6 +174,19 @@ def bdf_stats(reset: bool = True) -> dict:
     return {"steps": int(out[0]), "jacobians": int(out[1]), "groups": int(out[2])}
 
 
+def bdf_detail(reset: bool = True) -> dict:
+    """Per-phase counts of the BDF restatement since the last reset: accepted steps,
+    rejections on the error and on Newton, Newton iterations, order/step selections and grid
+    points emitted (where a BDF step's time goes; profiles/NOTES.md)."""
+    L = lib()
+    L.ref_bdf_detail.restype = None
+    L.ref_bdf_detail.argtypes = [C.c_void_p, C.c_int]
+    out = np.zeros(6, np.int64)
+    L.ref_bdf_detail(out.ctypes.data, int(reset))
+    return dict(zip(("accepted", "rejected_error", "rejected_newton", "newton_iterations", "selections",
+                     "grid_points"), (int(v) for v in out)))
+
+
 def inv_root(x: float, q: int) -> float:
     """x^(-1/q) as the BDF step controller computes it (oracle/rk_ref.c inv_root)."""
     return lib().ref_inv_root(float(x), int(q))
