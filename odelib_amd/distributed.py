@@ -90,11 +90,13 @@ def sharded_mh(engine, theta_all, y0_all, nits: int, burnin: int, walk_mask, ini
     return the pooled posterior samples [kept][P+5][W_total] (identical on all ranks).
     ``speculate``: each rank's speculative MH rounds (``Engine.mh_run``; on for shards too
     small to fill their device).  The draws are keyed by global walker id and iteration, so
-    with RK4 (every lane integrates alone) the pooled chains are bitwise those of one
-    sequential launch for any rank count.  With DOPRI5 / 'auto' a proposal shares its step
-    size with its lockstep group, which the sharding and the speculation depth (picked from
-    each rank's shard size and CU count) change: chi moves at the tolerance level, and a
-    decision whose margin |accp - u| is below ~1e-7 can flip (none in 576 restated chains,
+    with RK4 and DOPRI5 (every chain steps on its own in the MH kernels, csrc/lane.cuh) the
+    pooled chains are bitwise those of one sequential launch for any rank count (models of up
+    to 8 states; the split wide-chain kernels group 64/K chains per step size).  With 'auto',
+    proposals handed to BDF share that pass's step with the other handed proposals of their
+    wave, which the sharding and the speculation depth (picked from each rank's shard size and
+    CU count) change: chi moves at the tolerance level, and a decision whose margin |accp - u|
+    is below ~1e-7 can flip (none in 576 restated chains,
     tests/test_rkref_oracle.py::test_c_speculative_decision_agreement_over_many_chains) — the
     posterior is then the same distribution, not the same bits."""
     import torch.distributed as dist
