@@ -215,3 +215,23 @@ def test_split_dopri5_speculative_rounds(n, K):
     for k in ("samples", "theta", "y0", "final"):
         np.testing.assert_allclose(spec[k], ref[k], rtol=1e-8, err_msg=k)
     assert (seq["final"][3] > 0).any()
+
+
+@pytest.mark.parametrize("method", ["auto", "bdf"])
+def test_speculative_rounds_with_stiff_proposals_vs_c_restatement(method):
+    """Rounds whose proposals include stiff draws (tau = 1e5, 1e6 / lam = 1e4, 1e9): 'auto'
+    hands them to BDF from each lane's own eviction point, 'bdf' integrates every proposal
+    with it — the device rounds take the C restatement's decisions and values (rtol 1e-8, the
+    proposals' exp/log), status bitwise.  (The MH kernels sit at the register limit: this is
+    the case that caught a code-generation fragility of the BDF hand-over, lane.cuh.)"""
+    from test_gpu_stiff import _mixed_thetas
+    W = 128
+    m = product_model("two_i", method=method)
+    theta = _mixed_thetas("two_i", W, [1, 64, 65, 127])
+    y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+    walk = np.ones(5, np.uint8)
+    dev = _np(m.engine().mh_run(theta, y0, nits=4, burnin=0, walk_mask=walk, rng="philox", seed=11, speculate=3))
+    ref = rk_ref.mh_tree_run(m.fit_problem(), theta, y0, 4, 0, walk, depth=3, rng="philox", seed=11)
+    for k in ("samples", "theta", "final"):
+        np.testing.assert_allclose(dev[k], ref[k], rtol=1e-8, err_msg=k)
+    assert np.array_equal(dev["status"], ref["status"])
