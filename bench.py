@@ -672,18 +672,25 @@ def c4_leg(args, R, T, P):
     blk = r["samples"]
     res["posterior_block_bytes_per_rank"] = blk.numel() * 8
     pool = args.pool if (R.world == 1 or R.backend == "nccl") else "torch"
+    cabi_error = None
     if pool == "cabi":
-        from odelib_amd.distributed import native_allgather_walkers, native_comm
-        comm = native_comm(R.dev.index, None)
-        src = blk.contiguous()
-        native_allgather_walkers(src[:1], C4_WALKERS if R.world > 1 else cnt, comm)  # untimed: channel set-up
-        R.fence()
-        t0 = time.perf_counter()
-        pooled = native_allgather_walkers(src, C4_WALKERS if R.world > 1 else cnt, comm)
-        R.fence()
-        t_ag = R.max(time.perf_counter() - t0)
-        n_ranks = comm.n_ranks
-        comm.close()
+        try:
+            from odelib_amd.distributed import native_allgather_walkers, native_comm
+            comm = native_comm(R.dev.index, None)
+            src = blk.contiguous()
+            native_allgather_walkers(src[:1], C4_WALKERS if R.world > 1 else cnt, comm)  # untimed: channel set-up
+            R.fence()
+            t0 = time.perf_counter()
+            pooled = native_allgather_walkers(src, C4_WALKERS if R.world > 1 else cnt, comm)
+            R.fence()
+            t_ag = R.max(time.perf_counter() - t0)
+            n_ranks = comm.n_ranks
+            comm.close()
+        except Exception as e:  # an error raised by the C-ABI path (not a hang): pool with torch, say so
+            cabi_error = f"{type(e).__name__}: {e}"[:300]
+            pool = "torch"
+    if pool == "cabi":
+        pass
     elif R.world > 1:
         src = blk.contiguous() if R.backend == "nccl" else blk.cpu()
         allgather_walkers(src[:1], C4_WALKERS)  # untimed: communicator / channel set-up
@@ -702,10 +709,14 @@ def c4_leg(args, R, T, P):
                             "comm_n_ranks": n_ranks, "world_size": R.world, "bytes_gathered": gathered,
                             "s": t_ag, "algbw_GBps": gathered / t_ag / 1e9,
                             "busbw_GBps": gathered * (R.world - 1) / R.world / t_ag / 1e9}
+        if cabi_error:
+            res["allgather"]["cabi_error"] = cabi_error
         del pooled
     else:
         res["allgather"] = {"pool": "torch", "comm_n_ranks": 1, "world_size": 1,
                             "note": "one GPU, torch pooling: nothing to gather"}
+        if cabi_error:
+            res["allgather"]["cabi_error"] = cabi_error
     del r, blk
     torch.cuda.empty_cache()
     return res
