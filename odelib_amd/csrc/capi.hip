@@ -352,9 +352,9 @@ __global__ void __launch_bounds__(256) k_np_seed(const oe::NpState st, const uin
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w < W) oe::np_seed_lane(st, w, seeds[w]);
 }
-__global__ void __launch_bounds__(256) k_np_draws(const oe::NpDrawArgs d) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w < d.W) oe::np_draw_lane(d, w);
+static dim3 np_grid(int64_t W) { return dim3((unsigned)((W + oe::kNpChainsPerBlock - 1) / oe::kNpChainsPerBlock)); }
+__global__ void __launch_bounds__(oe::kNpChainsPerBlock) k_np_draws(const oe::NpDrawArgs d) {
+  oe::np_draw_block<oe::kNpChainsPerBlock>(d);
 }
 
 // MH proposal draws (philox mode), one lane per (walker, iteration) of the chunk: counter-
@@ -1122,7 +1122,7 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
     for (int f0 = 1; f0 < it_start; f0 += chunk) {  // resume: replay the consumed draws
       nd.it0 = f0;
       nd.it1 = std::min(it_start, f0 + chunk);
-      hipLaunchKernelGGL(k_np_draws, grid, block, 0, c->stream, nd);
+      hipLaunchKernelGGL(k_np_draws, np_grid(W), dim3(kNpChainsPerBlock), 0, c->stream, nd);
       OE_HIP(c, hipGetLastError());
     }
   }
@@ -1147,7 +1147,7 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       nd.it0 = m.it0;
       nd.it1 = m.it1;
       m.draw_it0 = it0;
-      hipLaunchKernelGGL(k_np_draws, grid, block, 0, c->stream, nd);
+      hipLaunchKernelGGL(k_np_draws, np_grid(W), dim3(kNpChainsPerBlock), 0, c->stream, nd);
       OE_HIP(c, hipGetLastError());
     }
     if (!depth) {
@@ -1211,7 +1211,7 @@ int oe_numpy_streams(oe_ctx* c, int64_t W, const uint32_t* seeds, int32_t nits, 
   OE_HIP(c, hipEventRecord(c->ev0, c->stream));
   hipLaunchKernelGGL(k_np_seed, grid, block, 0, c->stream, nd.st, seeds, W);
   OE_HIP(c, hipGetLastError());
-  hipLaunchKernelGGL(k_np_draws, grid, block, 0, c->stream, nd);
+  hipLaunchKernelGGL(k_np_draws, np_grid(W), dim3(kNpChainsPerBlock), 0, c->stream, nd);
   OE_HIP(c, hipGetLastError());
   OE_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;

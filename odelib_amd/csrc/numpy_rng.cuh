@@ -15,11 +15,14 @@
 // call; ocml and glibc agree to <= 1 ulp there, everything else is exact integer / IEEE
 // arithmetic (checked against numpy itself in tests/).
 //
-// MT state layout: key [W][624] (a chain's words contiguous, so successive draws of one
-// lane stay in the same cache lines), pos/gauss/has_gauss [W].  The twist is done lazily
-// one word per draw (word i of generation g+1 needs words i, i+1 of generation g and word
-// i+397 mod 624 of g or g+1 — exactly the values the block twist reads), so lanes whose
-// polar rejections differ never diverge into a 624-word loop.
+// MT state layout: key [W][624] in HBM (a chain's words contiguous), pos/gauss/has_gauss
+// [W].  A draw launch stages the keys of kNpChainsPerBlock chains through LDS, transposed
+// to [624][chains] so a wave's lanes at the same word index hit distinct banks, draws there
+// and writes them back: each 32-bit word costs LDS latency instead of a dependent global
+// load chain (r04: 299 -> see profiles/NOTES.md per chunk of the notebook fit).  The twist is
+// done lazily one word per draw (word i of generation g+1 needs words i, i+1 of generation g
+// and word i+397 mod 624 of g or g+1 — exactly the values the block twist reads), so lanes
+// whose polar rejections differ never diverge into a 624-word loop.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -48,20 +51,30 @@ struct NpDrawArgs {
   double* u;             // [it1 - it0][W]
 };
 
+constexpr int kNpChainsPerBlock = 64;  // 64 x 624 words = 156 KiB of LDS: one wave per CU
+
+// One chain's generator.  key[i * STRIDE] is word i (STRIDE = chains per block in LDS).
+// `nxt` carries word i+1 of the old generation from one draw to the next: it is the next
+// draw's word i and has not been overwritten in between (only word i is written per draw).
+template <int STRIDE>
 struct NpLane {
-  uint32_t* key;  // this chain's 624 words
+  uint32_t* key;
   int pos;
   double gauss;
   bool has_gauss;
+  uint32_t cur;  // key[pos] (old generation)
 
+  __device__ __forceinline__ void start() { cur = key[pos * STRIDE]; }
   __device__ __forceinline__ uint32_t next32() {
     const int i = pos;
     const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
     const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
-    const uint32_t y = (key[i] & 0x80000000u) | (key[i1] & 0x7fffffffu);
-    const uint32_t v = key[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    key[i] = v;
+    const uint32_t nxt = key[i1 * STRIDE];
+    const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+    const uint32_t v = key[im * STRIDE] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    key[i * STRIDE] = v;
     pos = i1;
+    cur = nxt;  // (at i = 623, word 0 is already the new generation's in both uses)
     uint32_t t = v;  // tempering
     t ^= t >> 11;
     t ^= (t << 7) & 0x9d2c5680u;
@@ -106,21 +119,43 @@ __device__ __forceinline__ void np_seed_lane(const NpState& st, int64_t w, uint3
   st.gauss[w] = 0.0;
 }
 
-__device__ __forceinline__ void np_draw_lane(const NpDrawArgs& d, int64_t w) {
+// The draws of chains [blockIdx.x * CPB, + CPB) with their keys staged in LDS; blockDim.x
+// == CPB.  Global <-> LDS copies are coalesced over the block's contiguous key region.
+template <int CPB>
+__device__ __forceinline__ void np_draw_block(const NpDrawArgs& d) {
+  __shared__ uint32_t sk[kMtN * CPB];
   const int64_t W = d.W;
-  NpLane L{d.st.key + w * kMtN, d.st.pos[w], d.st.gauss[w], d.st.has_gauss[w] != 0};
-  for (int it = d.it0; it < d.it1; ++it) {
-    double* dz = d.dz + (int64_t)(it - d.it0) * d.P * W + w;
-    for (int j = 0; j < d.P; ++j) {
-      if ((d.walk_mask >> j) & 1ull) dz[(int64_t)j * W] = 0.0 + d.step_sd * L.next_gauss();  // loc + scale*gauss
-      else if (d.zero_static) dz[(int64_t)j * W] = 0.0;
-    }
-    for (int k = 0; k < d.prior_draws; ++k) (void)L.next_gauss();
-    d.u[(int64_t)(it - d.it0) * W + w] = L.next_double();
+  const int64_t w0 = (int64_t)blockIdx.x * CPB;
+  const int nw = (int)((W - w0 < CPB) ? W - w0 : CPB);
+  uint32_t* gk = d.st.key + w0 * kMtN;
+  for (int r = threadIdx.x; r < nw * kMtN; r += CPB) {
+    const int c = r / kMtN, i = r - c * kMtN;
+    sk[i * CPB + c] = gk[r];
   }
-  d.st.pos[w] = L.pos;
-  d.st.gauss[w] = L.gauss;
-  d.st.has_gauss[w] = L.has_gauss ? 1 : 0;
+  __syncthreads();
+  const int c = threadIdx.x;
+  if (c < nw) {
+    const int64_t w = w0 + c;
+    NpLane<CPB> L{sk + c, d.st.pos[w], d.st.gauss[w], d.st.has_gauss[w] != 0, 0u};
+    L.start();
+    for (int it = d.it0; it < d.it1; ++it) {
+      double* dz = d.dz + (int64_t)(it - d.it0) * d.P * W + w;
+      for (int j = 0; j < d.P; ++j) {
+        if ((d.walk_mask >> j) & 1ull) dz[(int64_t)j * W] = 0.0 + d.step_sd * L.next_gauss();  // loc + scale*gauss
+        else if (d.zero_static) dz[(int64_t)j * W] = 0.0;
+      }
+      for (int k = 0; k < d.prior_draws; ++k) (void)L.next_gauss();
+      d.u[(int64_t)(it - d.it0) * W + w] = L.next_double();
+    }
+    d.st.pos[w] = L.pos;
+    d.st.gauss[w] = L.gauss;
+    d.st.has_gauss[w] = L.has_gauss ? 1 : 0;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < nw * kMtN; r += CPB) {
+    const int c2 = r / kMtN, i = r - c2 * kMtN;
+    gk[r] = sk[i * CPB + c2];
+  }
 }
 
 }  // namespace oe
