@@ -96,6 +96,11 @@ struct oe_ctx {
   size_t draws_bytes = 0;
   void* np_state = nullptr;  // numpy legacy RandomState per chain (key [W][624], pos, gauss, has)
   size_t np_state_bytes = 0;
+  // numpy draws of MH chunk j + 1 run on a side stream while chunk j's MH kernels run (one
+  // 64-chain block per CU beside them), into the other half of `draws`
+  hipStream_t np_stream = nullptr;
+  hipEvent_t ev_np[2] = {nullptr, nullptr};  // chunk j's draws written (side stream)
+  hipEvent_t ev_mh[2] = {nullptr, nullptr};  // chunk j's MH kernels done with buffer j & 1 (main)
   int32_t* stiff_buf = nullptr;  // wide-model stiff redo: [count][list W][status W]
   size_t stiff_cap = 0;          // walkers it holds
   void* tree = nullptr;          // speculative MH rounds: node proposals and results
@@ -178,6 +183,16 @@ int ensure_draws(oe_ctx* c, size_t bytes) {
   }
   OE_HIP(c, hipMalloc(&c->draws, bytes));
   c->draws_bytes = bytes;
+  return OE_OK;
+}
+
+int ensure_np_stream(oe_ctx* c) {
+  if (c->np_stream) return OE_OK;
+  OE_HIP(c, hipStreamCreateWithFlags(&c->np_stream, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k) {
+    OE_HIP(c, hipEventCreateWithFlags(&c->ev_np[k], hipEventDisableTiming));
+    OE_HIP(c, hipEventCreateWithFlags(&c->ev_mh[k], hipEventDisableTiming));
+  }
   return OE_OK;
 }
 
@@ -610,6 +625,14 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->tree) (void)hipFree(c->tree);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->np_stream) {
+      (void)hipStreamSynchronize(c->np_stream);
+      (void)hipStreamDestroy(c->np_stream);
+    }
+    for (int k = 0; k < 2; ++k) {
+      if (c->ev_np[k]) (void)hipEventDestroy(c->ev_np[k]);
+      if (c->ev_mh[k]) (void)hipEventDestroy(c->ev_mh[k]);
+    }
     for (auto& m : c->custom)
       for (hipModule_t md : {m->rtc.mod, m->rtc.stiff_mod})
         if (md) (void)hipModuleUnload(md);
@@ -1079,16 +1102,22 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   const bool philox = a->rng_mode == OE_RNG_PHILOX, numpy = a->rng_mode == OE_RNG_NUMPY;
   DrawArgs d{};
   NpDrawArgs nd{};
+  double* np_dz[2] = {nullptr, nullptr};
+  double* np_u[2] = {nullptr, nullptr};
   if ((philox || numpy) && a->nits > 1) {
     // one chunk of draws resident at a time, at most ~1 GiB (at least one iteration)
     const size_t per_it = sizeof(double) * (size_t)(P + 1) * (size_t)W;
     chunk = (int)std::max<int64_t>(1, std::min<int64_t>(chunk, (int64_t)((1ull << 30) / per_it)));
-    rc = ensure_draws(c, per_it * (size_t)chunk);
+    rc = ensure_draws(c, per_it * (size_t)chunk * (numpy ? 2 : 1));
     if (rc) return rc;
     double* dz = static_cast<double*>(c->draws);
     double* u = dz + (size_t)chunk * P * W;
     m.dz = dz;
     m.u = u;
+    np_dz[0] = dz;
+    np_u[0] = u;
+    np_dz[1] = dz + (size_t)chunk * (P + 1) * W;
+    np_u[1] = np_dz[1] + (size_t)chunk * P * W;
     if (philox) {
       d.W = W;
       d.walker_offset = a->walker_offset;
@@ -1109,6 +1138,8 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       nd.u = u;
       rc = ensure_np_state(c, W, &nd.st);
       if (rc) return rc;
+      rc = ensure_np_stream(c);
+      if (rc) return rc;
     }
   } else {
     m.dz = a->replay_dz;
@@ -1125,6 +1156,25 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       hipLaunchKernelGGL(k_np_draws, np_grid(W), dim3(kNpChainsPerBlock), 0, c->stream, nd);
       OE_HIP(c, hipGetLastError());
     }
+  }
+  // chunk j's numpy draws on the side stream, into buffer j & 1: after the MT state is ready
+  // (j = 0) and after chunk j - 2's MH kernels have read that buffer (j >= 2)
+  auto np_draws_chunk = [&](int j) -> int {
+    nd.it0 = it_start + j * chunk;
+    nd.it1 = std::min(a->nits, nd.it0 + chunk);
+    nd.dz = np_dz[j & 1];
+    nd.u = np_u[j & 1];
+    if (j >= 2) OE_HIP(c, hipStreamWaitEvent(c->np_stream, c->ev_mh[j & 1], 0));
+    hipLaunchKernelGGL(k_np_draws, np_grid(W), dim3(kNpChainsPerBlock), 0, c->np_stream, nd);
+    OE_HIP(c, hipGetLastError());
+    OE_HIP(c, hipEventRecord(c->ev_np[j & 1], c->np_stream));
+    return OE_OK;
+  };
+  if (numpy && a->nits > 1 && it_start < a->nits) {
+    OE_HIP(c, hipEventRecord(c->ev_mh[0], c->stream));  // seeded / replayed state
+    OE_HIP(c, hipStreamWaitEvent(c->np_stream, c->ev_mh[0], 0));
+    rc = np_draws_chunk(0);
+    if (rc) return rc;
   }
   if (!resume) {
     m.init = 1;
@@ -1144,37 +1194,43 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
                          c->stream, d);
       OE_HIP(c, hipGetLastError());
     } else if (numpy) {
-      nd.it0 = m.it0;
-      nd.it1 = m.it1;
+      const int j = (it0 - it_start) / chunk;
+      if (m.it1 < a->nits) {
+        rc = np_draws_chunk(j + 1);
+        if (rc) return rc;
+      }
+      OE_HIP(c, hipStreamWaitEvent(c->stream, c->ev_np[j & 1], 0));
+      m.dz = np_dz[j & 1];
+      m.u = np_u[j & 1];
       m.draw_it0 = it0;
-      hipLaunchKernelGGL(k_np_draws, np_grid(W), dim3(kNpChainsPerBlock), 0, c->stream, nd);
-      OE_HIP(c, hipGetLastError());
     }
     if (!depth) {
       OE_HIP(c, launch_mh(m));
-      continue;
-    }
-    for (int r0 = m.it0; r0 < m.it1; r0 += ta.depth) {
-      ta.m = m;
-      ta.m.it0 = r0;
-      ta.depth = std::min(depth, m.it1 - r0);
-      ta.n_lanes = ((int64_t(1) << ta.depth) - 1) * W;
-      const dim3 tgrid((unsigned)((ta.n_lanes * lanes_per_walker + kBlock - 1) / kBlock));
-      if (split) {
-        e->mh_split_tree(c->dp, ta, tgrid, block, c->stream);
+    } else {
+      for (int r0 = m.it0; r0 < m.it1; r0 += ta.depth) {
+        ta.m = m;
+        ta.m.it0 = r0;
+        ta.depth = std::min(depth, m.it1 - r0);
+        ta.n_lanes = ((int64_t(1) << ta.depth) - 1) * W;
+        const dim3 tgrid((unsigned)((ta.n_lanes * lanes_per_walker + kBlock - 1) / kBlock));
+        if (split) {
+          e->mh_split_tree(c->dp, ta, tgrid, block, c->stream);
+          OE_HIP(c, hipGetLastError());
+        } else {
+          OE_HIP(c, launch_mh_tree_entry(e, c->method, c->dp, ta, tgrid, block, c->stream));
+        }
+        // one wave per chain pays off for deep trees of few chains (32 chains, d = 11: 0.0311 ->
+        // 0.0287 ms per iteration); shallow trees of many chains keep one lane per chain
+        // (8 192 chains, d = 3: 0.079 vs 0.099)
+        if (ta.depth >= 5 && ta.depth <= kResolveLdsDepth)
+          hipLaunchKernelGGL(k_mh_resolve_wave, dim3((unsigned)W), dim3(64), 0, c->stream, c->dp, ta, (int32_t)S);
+        else
+          hipLaunchKernelGGL(k_mh_resolve, grid, block, 0, c->stream, c->dp, ta, (int32_t)S);
         OE_HIP(c, hipGetLastError());
-      } else {
-        OE_HIP(c, launch_mh_tree_entry(e, c->method, c->dp, ta, tgrid, block, c->stream));
       }
-      // one wave per chain pays off for deep trees of few chains (32 chains, d = 11: 0.0311 ->
-      // 0.0287 ms per iteration); shallow trees of many chains keep one lane per chain
-      // (8 192 chains, d = 3: 0.079 vs 0.099)
-      if (ta.depth >= 5 && ta.depth <= kResolveLdsDepth)
-        hipLaunchKernelGGL(k_mh_resolve_wave, dim3((unsigned)W), dim3(64), 0, c->stream, c->dp, ta, (int32_t)S);
-      else
-        hipLaunchKernelGGL(k_mh_resolve, grid, block, 0, c->stream, c->dp, ta, (int32_t)S);
-      OE_HIP(c, hipGetLastError());
     }
+    if (numpy && m.it1 < a->nits)  // buffer j & 1 is free for chunk j + 2's draws
+      OE_HIP(c, hipEventRecord(c->ev_mh[((it0 - it_start) / chunk) & 1], c->stream));
   }
   OE_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
