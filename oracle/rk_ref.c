@@ -30,6 +30,15 @@
 #include <string.h>
 
 #define LANES 64
+/* study knobs for the 'auto' hand-over (tools/demo_gate_study.py; the defaults are the
+   kernels'): NSW_RESUME = ode_kernels.cuh kBdfSwitchSteps; GATE_ALL = 1 runs the stiffness
+   test by steps since the start rather than since the last grid point */
+#ifndef NSW_RESUME
+#define NSW_RESUME 300.0
+#endif
+#ifndef GATE_ALL
+#define GATE_ALL 0
+#endif
 #ifndef BDF_SWITCH_LONG
 #define BDF_SWITCH_LONG 1500.0
 #endif
@@ -300,7 +309,7 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
   h = fmin(h, tend - t0);
   const double span = tend - t0;
   const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
-  int i = 1, nst = 0, last_rej = 0;
+  int i = 1, nst = 0, last_rej = 0, nst_all = 0;
   long long n_acc = 0, n_rej = 0;
   while (i < pb->T) {
     int last = 0;
@@ -359,16 +368,17 @@ static void dopri5_group(const Prob* pb, Lane* L, int nl, const double* p, doubl
     }
     double err = grp_max(L, nl, 1);
     ++nst;
+    ++nst_all;
     if (err <= 1.0) {
       /* cost gate (ode_kernels.cuh kStiffSwitchSteps / kStiffSwitchStepsSlow): tested only
          while the shared step is below (tend - t)/N */
-      const double nsw = resume ? 300.0 : (S <= 8 || pb->wave_redo) ? 4000.0 : 40000.0;
+      const double nsw = resume ? NSW_RESUME : (S <= 8 || pb->wave_redo) ? 4000.0 : 40000.0;
       const int ntest = resume ? 2 : 3; /* ode_kernels.cuh kBdfTestSteps / kStiffTestSteps */
       /* (h|lambda|)^2 above which a tested step counts as stiff: resume (S <= 8) 2.5^2 at the
          stability limit, or 0.5^2 while finishing at this step would take over 1500 more steps
          (accuracy-limited on a fast component, where BDF takes far fewer); otherwise 3.25^2 */
       const double thr2 = !resume ? 10.5625 : ((tend - t) > BDF_SWITCH_LONG * h) ? BDF_THR_LONG2 : 6.25;
-      if (autom && nst >= ntest && (tend - t) > nsw * h) { /* ode_kernels.cuh kBdfSwitchSteps */
+      if (autom && (resume && GATE_ALL ? nst_all : nst) >= ntest && (tend - t) > nsw * h) { /* ode_kernels.cuh kBdfSwitchSteps */
         for (int l = 0; l < nl; ++l) {
           Lane* q = &L[l];
           /* components weighted by 1/(atol + rtol·max(|y|,|ynew|)), the error scale */
