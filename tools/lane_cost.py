@@ -6,7 +6,9 @@ step counts of the C restatement (CPU) — is a demo step dearer than a syntheti
 Each case runs `nits` MH iterations whose proposals are the same θ every time (replay draws
 dz = 0, u = 2: never accepted), so every iteration integrates exactly the given 32 θ; the
 kernel time per iteration ÷ the slowest lane's steps (C restatement, lane mode) is the cost
-of one step of a 32-lane wave.
+of one step of a 32-lane wave.  The C counts come from `auto` lane mode for both kernels
+(identical to `dopri5`'s without a hand-over; `dopri5` lane mode's stats also count the idle
+padding lanes of a one-walker call).
 """
 import json
 import os
@@ -33,16 +35,16 @@ def main():
     for method in ("dopri5", "auto"):
         mm = bench.demo_model()
         mm.method = method
-        fp = mm.fit_problem()
-        fp.method = method
         eng = mm.engine() if hasattr(mm, "engine") else None
+        fpc = mm.fit_problem()
+        fpc.method = "auto"
         for name, th in cases.items():
             th = np.ascontiguousarray(th, dtype=float)
             steps = []
             for w in range(32):
                 rk_ref.dopri5_stats()
                 rk_ref.bdf_detail()
-                rk_ref.integrate(fp, y0[:, w:w + 1].copy(), th[:, w:w + 1].copy(), trajectory=False, lane=True)
+                rk_ref.integrate(fpc, y0[:, w:w + 1].copy(), th[:, w:w + 1].copy(), trajectory=False, lane=True)
                 s = rk_ref.dopri5_stats()
                 b = rk_ref.bdf_detail()
                 steps.append((s["accepted"] + s["rejected"], b["accepted"] + b["rejected_error"] + b["rejected_newton"]))
