@@ -1617,7 +1617,7 @@ __global__ void __launch_bounds__(256)
 // integration tolerance.  For W chains the round keeps (2^d - 1)·W lanes busy: with few
 // chains the GPU is mostly idle in k_mh, and d iterations cost about one.
 // Node n (heap order): depth j = floor(log2(n + 1)), path bits p = n + 1 - 2^j, bit k of p
-// = the decision at depth k; lane layout node-major, [n][W].
+// = the decision at depth k; buffers node-major, [n][W]; 'auto' lanes chain-major (k_mh_tree).
 // ---------------------------------------------------------------------------------
 struct MHTreeArgs {
   MHArgs m;            // chain state, draws, masks; m.it0 = the round's first iteration
@@ -1640,9 +1640,24 @@ __global__ void __launch_bounds__(256)
   const int P = pb.P;
   const int64_t gl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = gl < ta.n_lanes;
-  const int64_t g = active ? gl : ta.n_lanes - 1;
-  const int64_t n = g / W;
-  const int64_t c = g - n * W;
+  const int64_t gw = active ? gl : ta.n_lanes - 1;
+  // 'auto': chain-major lanes — a wave holds consecutive nodes of one chain, near-identical
+  // proposals that step alike, observe together at little cost and share the BDF pass's
+  // lockstep with proposals of the same stiffness (notebook fit, same box: 0.229 -> 0.221 s,
+  // 1 024 chains 0.706 -> 0.678 s); the other methods keep node-major lanes (a wave = 64 // W
+  // nodes of every chain: synthetic RK4 rounds 7-9 % faster that way, profiles/NOTES.md r04x).
+  // The node buffers are node-major (index g = n·W + c) either way.  n_lanes < 2^29.
+  int64_t n, c;
+  if constexpr (METHOD == kAuto) {
+    const uint32_t nodes = (uint32_t)(ta.n_lanes / W);
+    const uint32_t cq = (uint32_t)gw / nodes;
+    n = (int64_t)((uint32_t)gw - cq * nodes);
+    c = cq;
+  } else {
+    n = gw / W;
+    c = gw - n * W;
+  }
+  const int64_t g = n * W + c;
   const int j = 31 - __builtin_clz((uint32_t)(n + 1));  // depth
   const uint32_t path = (uint32_t)(n + 1) - (1u << j);
   const uint32_t off = (uint32_t)c * 8u;

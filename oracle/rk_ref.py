@@ -222,8 +222,9 @@ def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3
                 replay=None, step_sd=0.05, walker_offset=0, chunk=25, split=None):
     """The speculative MH rounds of oe_mh_run (oe_mh_args.speculate = depth; ode_kernels.cuh
     k_mh_tree / capi.hip k_mh_resolve) restated on top of this restatement's batched
-    integrate: per round of d iterations the (2^d - 1)·W proposals (node-major lanes, node n
-    at depth floor(log2(n+1)), path bits n + 1 - 2^depth) are integrated in ONE call —
+    integrate: per round of d iterations the (2^d - 1)·W proposals (node-major lanes n·W + c,
+    chain-major c·N + n for 'auto'; node n at depth floor(log2(n+1)), path bits
+    n + 1 - 2^depth) are integrated in ONE call —
     the same lockstep grouping as the device lanes — then each chain walks its tree with
     the accept test exp(log(exp(chi - chin))) > u (Samplers.py:124-153).  Rounds restart at
     the device's chunk boundaries (chunk rounded down to a multiple of d).  Proposals use
@@ -279,12 +280,18 @@ def mh_tree_run(fp, theta, y0, nits, burnin, walk_mask, init_param=None, depth=3
                 for s in range(S):
                     if ip[s] >= 0:
                         ys[:, s] = tn[:, ip[s]]
-            res = integrate(fp, np.ascontiguousarray(ys.transpose(1, 0, 2).reshape(S, N * W)),
-                            np.ascontiguousarray(tn.transpose(1, 0, 2).reshape(P, N * W)), trajectory=False,
-                            split=split, lane=lane)
-            nchi = res["chi"].reshape(N, W)
-            nss = res["ssres"].reshape(N, W)
-            nst = res["status"].reshape(N, W)
+            if split == 1 and pr.method == METHODS["auto"]:  # 'auto' k_mh_tree lanes: chain-major (c·N + n), 64 a group
+                res = integrate(fp, np.ascontiguousarray(ys.transpose(1, 2, 0).reshape(S, W * N)),
+                                np.ascontiguousarray(tn.transpose(1, 2, 0).reshape(P, W * N)), trajectory=False,
+                                split=split, lane=lane)
+                nchi, nss, nst = (res[k].reshape(W, N).T for k in ("chi", "ssres", "status"))
+            else:  # node-major lanes (the other methods; split.cuh's tree kernel)
+                res = integrate(fp, np.ascontiguousarray(ys.transpose(1, 0, 2).reshape(S, N * W)),
+                                np.ascontiguousarray(tn.transpose(1, 0, 2).reshape(P, N * W)), trajectory=False,
+                                split=split, lane=lane)
+                nchi = res["chi"].reshape(N, W)
+                nss = res["ssres"].reshape(N, W)
+                nst = res["status"].reshape(N, W)
             for w in range(W):
                 path = 0
                 for j in range(d):
