@@ -674,21 +674,39 @@ def c4_leg(args, R, T, P):
     pool = args.pool if (R.world == 1 or R.backend == "nccl") else "torch"
     cabi_error = None
     if pool == "cabi":
+        # Every rank takes the same path: the communicator set-up and the untimed first
+        # gather are agreed on by an all-reduce of an error flag before the timed gather,
+        # and its outcome after it — a rank that fell back alone would enter a different
+        # collective than its peers and the job would hang.
+        from odelib_amd.distributed import native_allgather_walkers, native_comm
+        comm, pooled = None, None
         try:
-            from odelib_amd.distributed import native_allgather_walkers, native_comm
-            comm = native_comm(R.dev.index, None)
-            src = blk.contiguous()
-            native_allgather_walkers(src[:1], C4_WALKERS if R.world > 1 else cnt, comm)  # untimed: channel set-up
-            R.fence()
-            t0 = time.perf_counter()
-            pooled = native_allgather_walkers(src, C4_WALKERS if R.world > 1 else cnt, comm)
-            R.fence()
-            t_ag = R.max(time.perf_counter() - t0)
-            n_ranks = comm.n_ranks
-            comm.close()
-        except Exception as e:  # an error raised by the C-ABI path (not a hang): pool with torch, say so
-            cabi_error = f"{type(e).__name__}: {e}"[:300]
-            pool = "torch"
+            try:
+                comm = native_comm(R.dev.index, None)
+                src = blk.contiguous()
+                native_allgather_walkers(src[:1], C4_WALKERS if R.world > 1 else cnt, comm)  # untimed: channel set-up
+                ok = 1.0
+            except Exception as e:  # an error raised by the C-ABI path (not a hang)
+                cabi_error, ok = f"{type(e).__name__}: {e}"[:300], 0.0
+            if -R.max(-ok) > 0.0:  # min over ranks: every rank set up its communicator
+                R.fence()
+                t0 = time.perf_counter()
+                try:
+                    pooled = native_allgather_walkers(src, C4_WALKERS if R.world > 1 else cnt, comm)
+                    ok = 1.0
+                except Exception as e:
+                    cabi_error, ok, pooled = f"{type(e).__name__}: {e}"[:300], 0.0, None
+                R.fence()
+                t_ag = R.max(time.perf_counter() - t0)
+                n_ranks = comm.n_ranks
+                if -R.max(-ok) == 0.0:
+                    pooled = None
+            if pooled is None:  # some rank failed: all pool with torch, and say so
+                cabi_error = cabi_error or "another rank's C-ABI pooling failed"
+                pool = "torch"
+        finally:
+            if comm is not None:
+                comm.close()
     if pool == "cabi":
         pass
     elif R.world > 1:

@@ -519,7 +519,10 @@ class ModelFramework:
         (new): the reference's chains print ``it exp(-chi)`` on every iteration
         (Samplers.py:123), chain after chain; pass False for large ensembles.
         ``speculate`` (new): speculative MH rounds while the chains leave the device idle
-        (``Samplers.batched_metropolis_hastings``); 0 = one iteration per step."""
+        (``Samplers.batched_metropolis_hastings``); 0 = one iteration per step.  Either way
+        the chains are the same bits on any device and rank count: every proposal is
+        integrated on its own (per-chain DOPRI5 steps, per-chain BDF steps and orders for
+        stiff proposals), as each reference chain runs its own odeint."""
         if isinstance(chain_inits, pd.DataFrame):
             chain_inits = [row.to_dict() for _, row in chain_inits[self.get_pnames()].iterrows()]
         if isinstance(chain_inits, int):

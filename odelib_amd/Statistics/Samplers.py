@@ -117,14 +117,12 @@ def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameter
              (MetropolisHastings with print_progress, Samplers.py:101-103).
     speculate : speculative MH rounds (``Engine.mh_run``): "auto" lets the library run
              several iterations per launch while the chains leave the device mostly idle
-             (a few to a few thousand chains); 0 runs one iteration per step.  RK4 and
-             DOPRI5 chains are bitwise the same either way (the MH kernels step every chain
-             on its own, csrc/lane.cuh).  'auto' too, except for proposals its stiffness test
-             hands to BDF: those share the BDF pass's step with the other handed proposals of
-             their wave, which speculation (and the depth the device's CU count selects)
-             changes — chi moves at the tolerance level and a decision with a margin below
-             ~1e-7 could flip (measured: none in 576 restated chains x 30 iterations,
-             tests/test_rkref_oracle.py); pass 0 for device-independent bits."""
+             (a few to a few thousand chains); 0 runs one iteration per step.  The chains
+             are bitwise the same either way, for every method: the MH kernels integrate
+             every proposal on its own (DOPRI5 step sizes per chain, csrc/lane.cuh; the BDF
+             hand-over of 'auto' and method 'bdf' with step sizes and orders per chain,
+             csrc/bdf_lane.cuh), so a chain does not depend on the chains that share its
+             wavefront, the speculation depth or the device's CU count."""
     m0 = chains[0]
     pnames = m0.get_pnames()
     snames = list(m0._snames)

@@ -105,6 +105,8 @@ struct oe_ctx {
   size_t stiff_cap = 0;          // walkers it holds
   void* tree = nullptr;          // speculative MH rounds: node proposals and results
   size_t tree_bytes = 0;
+  void* obs_buf = nullptr;       // MH 'auto' / 'bdf' (S <= 8): the per-lane BDF pass's deferred
+  size_t obs_bytes = 0;          // observations, [n_obs][lanes] (DevProblem::obs_c, bdf_lane.cuh)
   int32_t last_mh_depth = 0;     // iterations per round of the last oe_mh_run (0: sequential)
   // OE_TUNE: the RK4 trajectory kernel chosen per shape, with what was measured (built-in
   // models: in a process-wide table shared by every context on the device; hipRTC models here)
@@ -170,6 +172,19 @@ int ensure_scratch(oe_ctx* c, size_t bytes) {
   }
   OE_HIP(c, hipMalloc(&c->scratch, bytes));
   c->scratch_bytes = bytes;
+  return OE_OK;
+}
+
+int ensure_obs_buf(oe_ctx* c, size_t bytes) {
+  if (c->obs_bytes >= bytes) return OE_OK;
+  if (c->obs_buf) {
+    OE_HIP(c, hipStreamSynchronize(c->stream));
+    OE_HIP(c, hipFree(c->obs_buf));
+    c->obs_buf = nullptr;
+    c->obs_bytes = 0;
+  }
+  OE_HIP(c, hipMalloc(&c->obs_buf, bytes));
+  c->obs_bytes = bytes;
   return OE_OK;
 }
 
@@ -619,6 +634,7 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->d_obs) (void)hipFree(c->d_obs);
     if (c->d_rk4) (void)hipFree(c->d_rk4);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->obs_buf) (void)hipFree(c->obs_buf);
     if (c->draws) (void)hipFree(c->draws);
     if (c->np_state) (void)hipFree(c->np_state);
     if (c->stiff_buf) (void)hipFree(c->stiff_buf);
@@ -1090,6 +1106,15 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
         c->tree_bytes = bytes;
       }
     }
+  }
+  // the per-lane BDF pass (MH 'auto' / 'bdf', one lane per chain, S <= 8) defers its
+  // observations to a [n_obs][lanes] scratch: one column per lane of the largest launch
+  c->dp.obs_c = nullptr;
+  if (!split && (c->method == OE_METHOD_AUTO || c->method == OE_METHOD_BDF) && S <= 8 && c->dp.n_obs > 0) {
+    const int64_t lanes = depth ? ((int64_t(1) << depth) - 1) * W : W;
+    rc = ensure_obs_buf(c, sizeof(double) * (size_t)c->dp.n_obs * (size_t)lanes);
+    if (rc) return rc;
+    c->dp.obs_c = static_cast<double*>(c->obs_buf);
   }
   if (depth) {
     const int64_t nodes = (int64_t(1) << depth) - 1;

@@ -31,7 +31,6 @@
 
 namespace oe {
 
-constexpr int kGridWin = 8;  // the time grid buffer carries kGridWin + 1 +inf sentinels
 
 // AUTO (S <= kStiffRegS): the stiffness test of integrate_dopri5 hands the lane over at
 // its eviction point, as does the step budget; the BDF pass at the end continues it from
@@ -286,8 +285,7 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
   if constexpr (AUTO) {
     if (__ballot(handed) != 0ull) {  // wave-uniform: the BDF pass from each handed lane's (t, y, i, k)
       if (handed) a.status |= ST_STIFF;
-      integrate_bdf<M, PMAX, false, false>(pb, y, t, i, k_lane, p, nullptr, W, (int64_t)(off >> 3), active,
-                                           handed, a);
+      integrate_bdf_lane<M, PMAX>(pb, y, t, i, k_lane, p, W, (int64_t)(off >> 3), handed, a);
     }
   }
 }

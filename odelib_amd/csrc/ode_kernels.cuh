@@ -54,6 +54,8 @@ struct DevProblem {
   int32_t pnum;         // AIC parameter count
   double sstot;         // R² denominator
   double newton_tol;    // BDF Newton tolerance, max(10·eps/rtol, min(0.03, sqrt(rtol))) (host-computed)
+  double* obs_c;        // MH launches: [n_obs][lanes] scratch of the per-lane BDF pass's deferred
+                        // observations (bdf_lane.cuh); null elsewhere
 };
 
 enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8, ST_INTERNAL = 16 };
@@ -936,6 +938,10 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
 }  // namespace oe
 #include "stiff.cuh"
 #include "bdf.cuh"
+namespace oe {
+constexpr int kGridWin = 8;  // the time grid buffer carries kGridWin + 1 +inf sentinels (lane.cuh)
+}
+#include "bdf_lane.cuh"
 #include "lane.cuh"
 namespace oe {
 
@@ -948,13 +954,13 @@ namespace oe {
 #define OE_LANE_INTEGRATE 0
 #endif
 template <class M, int METHOD>
-constexpr bool kLaneSteps = (METHOD == kDOPRI5 || METHOD == kAuto) && M::S <= kStiffRegS;
+constexpr bool kLaneSteps = (METHOD == kDOPRI5 || METHOD == kAuto || METHOD == kBdf) && M::S <= kStiffRegS;
 
 template <class M, int PMAX, int METHOD, bool TRAJ, bool NT, bool WAVE_REDO = false, bool LANE = false>
 __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, int64_t w, bool active, Acc& a) {
-  static_assert(!LANE || (!TRAJ && kLaneSteps<M, METHOD>), "per-lane steps: no trajectory, DOPRI5/auto, S <= 8");
+  static_assert(!LANE || (!TRAJ && kLaneSteps<M, METHOD>), "per-lane steps: no trajectory, DOPRI5/auto/bdf, S <= 8");
   const uint32_t off = (uint32_t)w * 8u;  // byte offset of walker w in a [..][W] row
   if constexpr (METHOD == kRK4) {
     integrate_rk4<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
@@ -962,6 +968,10 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
     integrate_dopri5_lane<M, PMAX, false>(pb, y, p, W, off, active, a);
   } else if constexpr (METHOD == kDOPRI5 || M::S > kStiffMaxS) {
     integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
+  } else if constexpr (LANE && METHOD == kBdf) {  // MH kernels: BDF from t0, own h and q per lane
+    int k = 0;
+    emit<M::S, false, false>(pb, 0, y, nullptr, W, off, active, k, a);
+    integrate_bdf_lane<M, PMAX>(pb, y, kconst(pb.times)[0], 1, k, p, W, w, active, a);
   } else if constexpr (METHOD == kBdf) {  // LSODA's BDF branch for every walker (S <= kStiffRegS)
     static_assert(M::S <= kStiffRegS, "bdf: register path only");
     int k = 0;
@@ -1185,7 +1195,9 @@ __global__ void __launch_bounds__(512) k_integrate_dopri5_piped(const DevProblem
         ++i;
         ti = times[i];  // times[T] is the +inf sentinel
       }
-      if (ti == tn) {
+      // (i < T: an all-evicted wave publishes a last slot reaching t = +inf, and the
+      // sentinel times[T] = +inf equals it — that row would lie past the buffer)
+      if (i < T && ti == tn) {
         store_row_at<S, true, NT>(ia.traj + (int64_t)i * S * W, yn, W, off, active, a);
         ++i;
       }

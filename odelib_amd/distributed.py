@@ -89,16 +89,14 @@ def sharded_mh(engine, theta_all, y0_all, nits: int, burnin: int, walk_mask, ini
     ``group`` (each rank: its shard on its own device via ``engine``), Philox draws, and
     return the pooled posterior samples [kept][P+5][W_total] (identical on all ranks).
     ``speculate``: each rank's speculative MH rounds (``Engine.mh_run``; on for shards too
-    small to fill their device).  The draws are keyed by global walker id and iteration, so
-    with RK4 and DOPRI5 (every chain steps on its own in the MH kernels, csrc/lane.cuh) the
-    pooled chains are bitwise those of one sequential launch for any rank count (models of up
-    to 8 states; the split wide-chain kernels group 64/K chains per step size).  With 'auto',
-    proposals handed to BDF share that pass's step with the other handed proposals of their
-    wave, which the sharding and the speculation depth (picked from each rank's shard size and
-    CU count) change: chi moves at the tolerance level, and a decision whose margin |accp - u|
-    is below ~1e-7 can flip (none in 576 restated chains,
-    tests/test_rkref_oracle.py::test_c_speculative_decision_agreement_over_many_chains) — the
-    posterior is then the same distribution, not the same bits."""
+    small to fill their device).  The draws are keyed by global walker id and iteration, and
+    in the MH kernels every chain is integrated on its own — DOPRI5 step sizes per chain
+    (csrc/lane.cuh) and, for 'auto' / 'bdf', BDF step sizes and orders per chain
+    (csrc/bdf_lane.cuh) — so with RK4, DOPRI5, 'auto' and 'bdf' the pooled chains are bitwise
+    those of one sequential launch for any rank count and speculation depth (models of up to
+    8 states; the split wide-chain kernels group 64/K chains per step size), as the
+    reference's chains, one odeint call per proposal (Framework.py:656, :779-780), never
+    depend on each other."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     W = int(np.asarray(theta_all).shape[1]) if not hasattr(theta_all, "shape") else int(theta_all.shape[1])

@@ -69,9 +69,9 @@ typedef struct {
   int split;     /* DOPRI5 with a walker over `split` lanes (odelib_amd/csrc/split.cuh): groups of
                     64/split walkers share a step size; a walker's error norm is the argmax over
                     each lane's states, combined in a tree of lanes (lower lane kept on ties) */
-  int lane_steps; /* DOPRI5 / 'auto' without a trajectory, S <= 8 (odelib_amd/csrc/lane.cuh, the MH
-                     kernels): every walker takes its own step sizes, i.e. the lockstep algorithm
-                     on a group of one; the BDF pass of 'auto' stays one group of 64 */
+  int lane_steps; /* DOPRI5 / 'auto' / 'bdf' without a trajectory, S <= 8 (odelib_amd/csrc/lane.cuh and
+                     bdf_lane.cuh, the MH kernels): every walker takes its own step sizes and BDF
+                     orders, i.e. the lockstep algorithms on a group of one */
 } Prob;
 
 static void rhs(const Prob* pb, const double* y, double t, const double* ps, double* dy) {
@@ -1287,7 +1287,14 @@ static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double*
       any |= L[l].part;
       if (L[l].part) L[l].a.status |= ST_STIFF;
     }
-    if (any) bdf_group(pb, L, nl, p, traj, W);
+    if (any) {
+      if (pb->lane_steps) {
+        for (int l = 0; l < nl; ++l)
+          if (L[l].part) bdf_group(pb, L + l, 1, p + l * MAXP, traj, W);
+      } else {
+        bdf_group(pb, L, nl, p, traj, W);
+      }
+    }
     return;
   }
   for (int l = 0; l < nl; ++l) memcpy(L[l].y0c, L[l].y, sizeof(double) * S);
@@ -1373,7 +1380,12 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
       q->i_ev = 1;
       q->k_ev = q->kobs;
     }
-    bdf_group(pb, L, LANES, p, traj, W);
+    if (pb->lane_steps) {
+      for (int l = 0; l < LANES; ++l)
+        if (L[l].part) bdf_group(pb, L + l, 1, p + l * MAXP, traj, W);
+    } else {
+      bdf_group(pb, L, LANES, p, traj, W);
+    }
   } else {
     for (int l = 0; l < LANES; ++l) L[l].part = L[l].active;
     if (pb->wave_redo) {
@@ -1393,7 +1405,9 @@ int ref_integrate(int model, int S, int P, int T, const double* times, int n_obs
                   int lane_steps) {
   if (S > MAXS || P > MAXP || W <= 0) return -1;
   if (split > 1 && (method != METHOD_DOPRI5 || split > 4 || S % split)) return -1;
-  if (lane_steps && (traj || split > 1 || S > 8 || (method != METHOD_DOPRI5 && method != METHOD_AUTO))) return -1;
+  if (lane_steps && (traj || split > 1 || S > 8 || (method != METHOD_DOPRI5 && method != METHOD_AUTO &&
+                                                      method != METHOD_BDF)))
+    return -1;
   Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
   pb.wave_redo = S > 8; /* ode_kernels.cuh kStiffRegS */
   pb.split = split;
@@ -1469,7 +1483,7 @@ int ref_mh(int model, int S, int P, int T, const double* times, int n_obs, const
   Prob pb = make_prob(model, S, P, T, times, n_obs, tidx, mask, O, two_s2, lin, method, substeps, rtol, atol, max_steps);
   pb.split = split; /* the split MH kernel (split.cuh k_mh_split): 64/split walkers per step size */
   /* the one-lane MH kernels step every chain on its own (ode_kernels.cuh kLaneSteps) */
-  pb.lane_steps = split <= 1 && S <= 8 && (method == METHOD_DOPRI5 || method == METHOD_AUTO);
+  pb.lane_steps = split <= 1 && S <= 8 && (method == METHOD_DOPRI5 || method == METHOD_AUTO || method == METHOD_BDF);
   const int G = group_size(&pb);
   int any_walk = 0;
   for (int j = 0; j < P; ++j) any_walk |= walk[j] != 0;

@@ -101,8 +101,9 @@ def product_split(fp) -> int:
 
 def lane_steps(fp) -> bool:
     """Whether the product's MH kernels step every chain on its own (ode_kernels.cuh
-    kLaneSteps, lane.cuh): DOPRI5 / 'auto', one lane per walker, at most 8 states."""
-    return fp.method in ("dopri5", "auto") and int(fp.n_states) <= 8 and product_split(fp) == 1
+    kLaneSteps, lane.cuh, bdf_lane.cuh): DOPRI5 / 'auto' / 'bdf', one lane per walker, at most
+    8 states — step sizes (and BDF orders) per walker, not per lockstep group."""
+    return fp.method in ("dopri5", "auto", "bdf") and int(fp.n_states) <= 8 and product_split(fp) == 1
 
 
 def integrate(fp, y0, theta, trajectory=True, split=None, lane=False):

@@ -49,6 +49,25 @@ def test_piped_dopri5_evicted_lanes_and_all_dead_wave():
     _assert_same(a, b)
 
 
+def test_piped_dopri5_all_dead_wave_stays_inside_the_buffer():
+    """The all-evicted wave's last slot reaches t = +inf, which the sentinel times[T] equals:
+    the store wave must not write a row T.  A canary row after the trajectory stays as it
+    was."""
+    import torch
+
+    m = product_model("two_i", method="dopri5")
+    theta = walker_thetas("two_i", 1, seed=2).T.copy()
+    theta[4, 0] = 1e9
+    eng = m.engine()
+    T, S = eng.problem.n_times, eng.problem.n_states
+    y0 = np.asarray(m.get_inits(), float)[:, None].copy()
+    for kernel in (None, "pipe2"):
+        buf = torch.full((T + 1, S, 1), 12345.0, dtype=torch.float64, device=eng.dev)
+        out = eng.integrate(y0, theta, trajectory=True, traj_out=buf[:T], kernel=kernel)
+        assert (out["status"].cpu().numpy()[0] & 4), kernel
+        assert (buf[T].cpu().numpy() == 12345.0).all(), kernel
+
+
 @pytest.mark.parametrize("name", ["zero_i", "one_i"])
 def test_piped_dopri5_other_models(name):
     m = product_model(name, method="dopri5")
