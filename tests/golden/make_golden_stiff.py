@@ -19,6 +19,14 @@ Draws (two_i, the notebook's 4-state model):
     region (phi = 1.06e-4, the host infected within ~1e-3 time units), where LSODA runs BDF.
 Stored (numbers only): theta, trajectories [W][T][S] (states before summation), the
 predictions at the observations, chi, R², AIC, per tolerance.
+
+Metropolis–Hastings chains in the stiff region (mh_stiff.npz + mh_stiff.json): the
+reference's own ``Statistics.Samplers.MetropolisHastings`` (Samplers.py:53-174: LSODA for
+every proposal, Framework.py:656; its global numpy stream seeded with random_seed) from the
+notebook fit's slow starts — phi ~ 1.5e-5, beta ~ 50 (where the fit's LHS survey starts its
+slowest chains) and tau = 1e3 — with the notebook's priors, 200 iterations each.  Stored:
+the posterior columns, and from the oracle's restatement of the same chains (bit-equal to
+the reference's, asserted here) each iteration's decision and margin acc − u.
 """
 from __future__ import annotations
 
@@ -72,9 +80,49 @@ def run(ODElib, m, TH, tol):
                 aic=np.array(aics))
 
 
+# (key, start, random_seed, nits): the notebook fit's slow region and a tau = 1e3 start
+MH_STIFF = [
+    ("slow_phi1.5e-5_s11", {"mu": 6.1e-9, "phi": 1.5e-5, "beta": 50.0, "lam": 2.0, "tau": 3.0}, 11, 200),
+    ("slow_phi1.2e-5_s12", {"mu": 8.0e-9, "phi": 1.2e-5, "beta": 55.0, "lam": 1.5, "tau": 2.5}, 12, 200),
+    ("tau1e3_s13", dict(THETA["two_i"], tau=1e3), 13, 200),
+]
+
+
+def mh_chains(ODElib):
+    import contextlib
+    import io
+    import json
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    sys.path.insert(0, os.path.dirname(HERE))
+    from helpers import oracle_model  # noqa: E402
+    from oracle import cpu_ref  # noqa: E402
+    out, meta = {}, {}
+    for key, th, seed, nits in MH_STIFF:
+        m = build_model(ODElib, "two_i", theta=th, seed=seed)
+        with contextlib.redirect_stdout(io.StringIO()):
+            post = ODElib.Statistics.Samplers.MetropolisHastings(m, nits=nits, print_progress=False)
+        ref = cpu_ref.metropolis_hastings(oracle_model("two_i", theta=th, seed=seed), nits=nits)
+        for c in post.columns:
+            v = np.asarray(post[c].to_numpy(), dtype=float)
+            assert np.array_equal(v, np.asarray(ref[c], dtype=float), equal_nan=True), (key, c)
+            out[f"{key}/{c}"] = v
+        out[f"{key}/margin"] = np.asarray(ref["margin"], dtype=float)
+        out[f"{key}/accepted"] = np.asarray(ref["accepted"], dtype=float)
+        meta[key] = dict(model="two_i", theta=th, seed=seed, nits=nits, columns=list(post.columns),
+                         accept_ratio=float(post["acceptance_ratio"].to_numpy()[-1]))
+    np.savez_compressed(os.path.join(HERE, "mh_stiff.npz"), **out)
+    with open(os.path.join(HERE, "mh_stiff.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("stiff MH chains written:", meta)
+
+
 def main():
     ODElib = import_reference()
     warnings.filterwarnings("ignore")
+    if "--mh-only" in sys.argv:
+        mh_chains(ODElib)
+        return
+    mh_chains(ODElib)
     m = build_model(ODElib, "two_i")
     out = {}
     near = walker_thetas("two_i", W=16, seed=1)

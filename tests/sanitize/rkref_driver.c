@@ -1,6 +1,8 @@
 /* TEST INFRASTRUCTURE: drives the C restatement (oracle/rk_ref.c) under AddressSanitizer
- * and UndefinedBehaviorSanitizer: every method (RK4, DOPRI5, auto,
- * Rosenbrock), the register path (two_i) and the wide path (chain20: private-memory
+ * and UndefinedBehaviorSanitizer, and under MemorySanitizer (uninitialised reads; clang,
+ * build/rkref_msan): every method (RK4, DOPRI5, auto,
+ * Rosenbrock, BDF — the lockstep group and the per-lane pass of the MH kernels' lane mode,
+ * at S = 4 and S = 8), the register path (two_i, chain8) and the wide path (chain20: private-memory
  * Rosenbrock, one walker per group), ragged walker counts, stiff / NaN / negative
  * walkers (a small step budget, so the eviction path runs), the batched MH with Philox and replay draws and a linked '<state>0'
  * parameter.  Any sanitizer report aborts the run (-fno-sanitize-recover). */
@@ -58,7 +60,7 @@ static void run_case(int model, int S, int P, int64_t W, int method, int with_tr
   int rc = ref_integrate(model, S, P, T, times, NOBS, tidx, mask, O, two_s2, lin, method, 2, 1.49012e-8, 1.49012e-8,
                          60, W, y0, th, traj, chi, ss, st, split,
                          /* without a trajectory: the MH kernels' per-lane DOPRI5 (lane.cuh) */
-                         !with_traj && split <= 1 && S <= 8 && (method == 1 || method == 2));
+                         !with_traj && split <= 1 && S <= 8 && (method == 1 || method == 2 || method == 4));
   if (rc) { fprintf(stderr, "ref_integrate rc=%d (model %d S %d method %d)\n", rc, model, S, method); exit(1); }
   /* Metropolis-Hastings: Philox, then replay with a linked initial state (P + 1) */
   const int nits = 9, burnin = 3, kept = nits - 1 - burnin;
@@ -102,9 +104,13 @@ int main(void) {
     two_s2[k] = 2.0 * 0.1 * 0.1;
     lin[k] = exp(O[k]);
   }
-  for (int method = 0; method < 4; ++method) {
+  for (int method = 0; method < 5; ++method) {
     run_case(2, 4, 5, method == 3 ? 12 : 70, method, 1, 0);  /* two_i: ragged groups (Rosenbrock: one) */
-    run_case(2, 4, 5, 3, method, 0, 0);     /* one partial group, chi only */
+    run_case(2, 4, 5, method == 3 ? 3 : 70, method, 0, 0);   /* chi only: the MH kernels' lane mode */
+  }
+  for (int method = 2; method <= 4; method += 2) {          /* chain8 'auto' / 'bdf': S = 8 */
+    run_case(3, 8, 5, 70, method, 1, 0);    /* lockstep groups (trajectory) */
+    run_case(3, 8, 5, 70, method, 0, 0);    /* lane mode (per-lane BDF) */
   }
   run_case(3, 20, 5, 66, 1, 1, 0);          /* chain20 DOPRI5 */
   run_case(3, 20, 5, 66, 1, 1, 2);          /* chain20 DOPRI5, split over 2 lanes (32-walker groups) */

@@ -68,3 +68,43 @@ def test_device_vs_reference_fixtures(golden, fx, method, group):
     assert np.array_equal(ours_ok, ref_ok)
     if group == "stiff" and method == "auto":
         assert (st & 8).all(), st               # every stiff draw handed to BDF
+
+
+def _mh_stiff():
+    import json
+    with open(os.path.join(GOLDEN, "mh_stiff.json")) as f:
+        meta = json.load(f)
+    return meta, dict(np.load(os.path.join(GOLDEN, "mh_stiff.npz")))
+
+
+@pytest.mark.parametrize("speculate", [0, "auto"])
+@pytest.mark.parametrize("key", ["slow_phi1.5e-5_s11", "slow_phi1.2e-5_s12", "tau1e3_s13"])
+def test_dropin_default_mh_vs_reference_stiff_region_chain(key, speculate):
+    """The reference's own MetropolisHastings chains from the notebook fit's slow starts
+    (phi ~ 1.5e-5, beta ~ 50: LSODA runs BDF on these proposals) and from tau = 1e3
+    (tests/golden/mh_stiff.npz, make_golden_stiff.py), replayed through the drop-in DEFAULT
+    path — method 'auto' at odeint's own tolerance, the reference's numpy stream — one
+    iteration per step and in speculative rounds.  Bars (written here): every accept decision
+    whose margin |acc − u| exceeds 1e-6 is the reference's (all 199 per chain are; the
+    smallest is 2.7e-3), and every kept row is within rtol 1e-5 of the reference's."""
+    from odelib_amd.Statistics import Samplers
+    meta, fx = _mh_stiff()
+    cfg = meta[key]
+    margins = fx[f"{key}/margin"]
+    decisive = np.abs(np.nan_to_num(margins, nan=1.0)) > 1e-6
+    n_ok = int(np.argmin(decisive)) if not decisive.all() else len(margins)
+    m = product_model(cfg["model"], theta=cfg["theta"], seed=cfg["seed"])
+    assert m.method == "auto"
+    post = Samplers.batched_metropolis_hastings([m], nits=cfg["nits"], speculate=speculate)
+    burnin = cfg["nits"] // 2
+    rows = max(0, n_ok - burnin)
+    assert rows == cfg["nits"] - 1 - burnin == len(post)
+    for c in cfg["columns"]:
+        np.testing.assert_allclose(post[c].to_numpy(dtype=float)[:rows], fx[f"{key}/{c}"][:rows], rtol=1e-5,
+                                   err_msg=c)
+    # the chain's proposals are stiff: 'auto' hands the start itself to BDF
+    eng = m.engine()
+    th0 = np.array([[cfg["theta"][p]] for p in m.get_pnames()])
+    r = eng.mh_run(th0, np.asarray(m.get_inits(), float)[:, None], nits=1, burnin=0,
+                   walk_mask=np.ones(len(th0), np.uint8))
+    assert int(r["status"].cpu().numpy()[0]) & 8

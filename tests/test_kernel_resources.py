@@ -4,7 +4,9 @@ A kernel that starts spilling is still bitwise correct, so parity tests do not s
 the chain20 DOPRI5 MH kernel once doubled in time (13.4 vs 6.3 ms per iteration,
 DESIGN.md §3.4 r01k) after unrelated integrator changes pushed it to 432 B/lane of
 scratch.  These budgets catch that at build time: hipcc's kernel-resource-usage remarks
-for the two translation units the bench and the C3 configs use.
+for the translation units the bench and the C3 configs use, and for the stiff methods' MH
+kernels (k_mh / k_mh_tree with 'auto' and 'bdf', the per-lane BDF pass of csrc/bdf_lane.cuh)
+of every built-in model with at most 8 states.
 """
 import os
 import re
@@ -15,8 +17,10 @@ import pytest
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "odelib_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950", "--cuda-device-only",
          "-Rpass-analysis=kernel-resource-usage", "-c", "-o", os.devnull]
+SMALL_UNITS = ["inst_zero_i.hip", "inst_one_i.hip", "inst_two_i.hip", "inst_chain4.hip"]  # S <= 4
+WIDE_REG_UNITS = ["inst_chain5.hip", "inst_chain6.hip", "inst_chain8.hip"]  # the register path's widest
 
 _FIELDS = {"VGPRs": "vgpr", "AGPRs": "agpr", "ScratchSize [bytes/lane]": "scratch",
            "Occupancy [waves/SIMD]": "occupancy", "SGPRs Spill": "sgpr_spill", "VGPRs Spill": "vgpr_spill"}
@@ -39,7 +43,7 @@ def _parse(text):
 def resources():
     if not os.path.exists(HIPCC) and shutil.which("hipcc") is None:
         pytest.skip("hipcc not available")
-    units = ["inst_two_i.hip", "inst_chain20.hip"]
+    units = sorted(set(SMALL_UNITS + WIDE_REG_UNITS + ["inst_chain20.hip"]))
     procs = {u: subprocess.Popen([HIPCC, *FLAGS, u], cwd=CSRC, stdout=subprocess.PIPE,
                                  stderr=subprocess.STDOUT, text=True) for u in units}
     out = {}
@@ -90,3 +94,29 @@ def test_chain20_rk4_kernels_fit_registers(resources):
 def test_chain20_dopri5_mh_scratch_budget(resources):
     r = _find(resources["inst_chain20.hip"], *MH_CHAIN20_DOPRI5)
     assert r["scratch"] <= 192, r  # 160 B/lane at r01k; 432 when it ran 2x slower
+
+
+def _stiff_mh(kernels):
+    """k_mh / k_mh_tree with METHOD 2 ('auto') or 4 ('bdf')"""
+    return {k: v for k, v in kernels.items() if re.search(r"k_mh(_tree)?I.*ELi[24]EEEv", k)}
+
+
+@pytest.mark.parametrize("unit", SMALL_UNITS)
+def test_small_models_never_spill(resources, unit):
+    """Up to 4 states every kernel — the 'auto' / 'bdf' MH kernels with the per-lane BDF
+    pass included — runs without scratch."""
+    ks = resources[unit]
+    assert len(_stiff_mh(ks)) == 4, list(ks)
+    for name, r in ks.items():
+        assert r["scratch"] == 0, (name, r)
+
+
+@pytest.mark.parametrize("unit", WIDE_REG_UNITS)
+def test_stiff_mh_kernels_scratch_budget_up_to_8_states(resources, unit):
+    """5..8 states: the per-lane BDF pass (difference table in LDS, LU in registers) keeps the
+    'auto' / 'bdf' MH kernels within 256 B/lane of scratch (chain8 'auto' k_mh was 1 296-1 376
+    with the lockstep pass; 80 now)."""
+    ks = _stiff_mh(resources[unit])
+    assert len(ks) == 4, list(resources[unit])
+    for name, r in ks.items():
+        assert r["scratch"] <= 256, (name, r)

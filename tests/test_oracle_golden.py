@@ -131,3 +131,28 @@ def test_stiff_and_near_posterior_fixtures_bit_exact(group, tag, tol):
         assert np.array_equal(np.concatenate([d[s] for s in d]), fx[f"{group}/{tag}/pred"][w])
         assert float(m.get_chi(d)) == fx[f"{group}/{tag}/chi"][w]
         assert float(m.get_Rsqrd(d)) == fx[f"{group}/{tag}/rsq"][w]
+
+
+def _mh_stiff():
+    import json
+    import os
+
+    from helpers import GOLDEN
+    with open(os.path.join(GOLDEN, "mh_stiff.json")) as f:
+        meta = json.load(f)
+    return meta, dict(np.load(os.path.join(GOLDEN, "mh_stiff.npz")))
+
+
+@pytest.mark.parametrize("key", ["slow_phi1.5e-5_s11", "slow_phi1.2e-5_s12", "tau1e3_s13"])
+def test_stiff_region_metropolis_hastings_bit_exact(key):
+    """tests/golden/mh_stiff.npz (make_golden_stiff.py: the reference's MetropolisHastings,
+    LSODA for every proposal, from the notebook fit's slow starts phi ~ 1.5e-5 / beta ~ 50
+    and from tau = 1e3, 200 iterations, seeded numpy stream): the oracle's chain is the
+    reference's, every column bit for bit, and its stored decision margins are the oracle's."""
+    meta, fx = _mh_stiff()
+    cfg = meta[key]
+    ref = cpu_ref.metropolis_hastings(oracle_model(cfg["model"], theta=cfg["theta"], seed=cfg["seed"]),
+                                      nits=cfg["nits"])
+    for c in cfg["columns"]:
+        assert np.array_equal(np.asarray(ref[c], float), fx[f"{key}/{c}"], equal_nan=True), c
+    assert np.array_equal(np.asarray(ref["margin"], float), fx[f"{key}/margin"], equal_nan=True)

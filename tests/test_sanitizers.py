@@ -3,6 +3,10 @@
 * the C restatement (oracle/rk_ref.c) under ASan + UBSan + LeakSanitizer: every method,
   the register and wide stiff paths, ragged groups, stiff / NaN / negative walkers, MH
   with Philox and replay draws (tests/sanitize/rkref_driver.c);
+* the same driver under MemorySanitizer (clang, origins tracked): no uninitialised read in
+  the restated algorithms — the lockstep BDF group and the MH kernels' per-lane BDF at
+  S = 4 and 8 included — so a device result that depends on code shape is not an
+  algorithm reading undefined state (profiles/NOTES.md, round 5);
 * the C-ABI's host code (capi/rtc/comm built with host-side ASan + UBSan, device code as
   shipped): validation and error paths and a hipRTC compile on the CPU; the full device
   path (every method, MH in every RNG mode, resume, a run-time compiled model with its
@@ -30,6 +34,12 @@ def _exe(name):
 def test_rk_ref_under_asan_ubsan_lsan():
     env = dict(ENV, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", OMP_NUM_THREADS="2")
     r = subprocess.run([_exe("rkref_asan")], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "SANITIZE OK" in r.stdout, r.stderr[-4000:]
+
+
+def test_rk_ref_under_msan():
+    r = subprocess.run([_exe("rkref_msan")], env=dict(os.environ, MSAN_OPTIONS="halt_on_error=1"),
+                       capture_output=True, text=True, timeout=400)
     assert r.returncode == 0 and "SANITIZE OK" in r.stdout, r.stderr[-4000:]
 
 
