@@ -3,9 +3,13 @@
 // form of scipy's BDF solver (the NDF scheme of Shampine & Reichelt with scipy's kappa table),
 // with the max norm LSODA uses and a modified Newton iteration: the LU factors of I − c·J are
 // kept across steps and rebuilt, from a fresh Jacobian, when the step size or the order
-// changes or Newton fails on factors from an earlier step.
+// changes or Newton fails on factors from an earlier step.  (Jacobian: scipy's BDF keeps J
+// across step-size and order changes and refactors only I − c·J; LSODA re-evaluates J when
+// the step size changes by more than 30 % (ccmax 0.3) and every 20 steps.  Here J is taken
+// afresh with each new factorisation — no J is kept, S² doubles fewer per lane — which sits
+// between the two; parity with the reference is to its tolerance, not its step counts.)
 //
-// Why BDF and not the Rosenbrock method for the walkers 'auto' hands over (DESIGN.md §3.6):
+// Why BDF and not the Rosenbrock method for the walkers 'auto' hands over (DESIGN.md §3.4):
 // LSODA switches to BDF, and on the draws that make the reference's fits expensive the two
 // differ by an order of magnitude.  A stiff component sitting on its quasi-steady state
 // (two_i's I1 at τ = 1e4: I1 ≈ φ·S·V/τ) drives a one-step Rosenbrock method into order
@@ -13,35 +17,15 @@
 // error on it is the smooth (q+1)-th difference: 550-650 BDF steps, each ~2.4 RHS
 // evaluations and 1/5 of an LU factorisation (scipy's BDF: 546; LSODA: 734).
 //
-// Lockstep layout: the lanes that take part carry their OWN time t (a lane joins at its
-// DOPRI5 eviction point) but share the step size h and the order q (wave decisions from
-// wave-max norms), so every vector operation is uniform; only the dense output onto each
-// lane's own grid points diverges.  Steps may end past t_end (as LSODA's itask = 1
-// overshoot), the grid points come from the backward-difference interpolant.
-//
 // Everything is IEEE add/mul/fma/div plus frexp/ldexp, restated operation for operation in
-// oracle/rk_ref.c (bdf_group), so the kernel is bitwise testable.
+// oracle/rk_ref.c (bdf_group on a group of one), so the kernels are bitwise testable.
 #pragma once
 
 namespace oe {
 namespace bdf {
 constexpr int kMaxQ = 5;
-constexpr int kRows = kMaxQ + 3;  // D[0..q+2]
 constexpr int kNewtonMaxIter = 4;
 constexpr int kBudget = 8;  // steps per output interval, in units of max_steps
-// scipy's BDF tables: gamma_q = Σ_{j<=q} 1/j, alpha_q = (1 − kappa_q)·gamma_q (1/alpha here),
-// error constants kappa_q·gamma_q + 1/(q+1), Newton-count safety 0.9·(2·4+1)/(2·4+n)
-__device__ const double kGamma[6] = {0.0, 1.0, 1.5, 1.8333333333333333, 2.083333333333333, 2.283333333333333};
-__device__ const double kInvAlpha[6] = {0.0, 0.8438818565400843, 0.6, 0.5039772202296456, 0.4608737397983678,
-                                        0.43795620437956206};
-__device__ const double kEc[6] = {1.0, 0.315, 0.16666666666666666, 0.09911666666666669, 0.11354166666666668,
-                                  0.16666666666666666};
-__device__ const double kSafety[5] = {0.0, 0.8999999999999999, 0.8099999999999999, 0.7363636363636363,
-                                      0.6749999999999999};
-__device__ const double kInvI[6] = {0.0, 1.0, 0.5, 0.3333333333333333, 0.25, 0.2};
-// U of scipy's change_D (R(q, 1)): U[m][j] = (−1)^m·C(j, m), exact integers
-__device__ const double kU[6][6] = {{1, 1, 1, 1, 1, 1},    {0, -1, -2, -3, -4, -5}, {0, 0, 1, 3, 6, 10},
-                                    {0, 0, 0, -1, -4, -10}, {0, 0, 0, 0, 1, 5},      {0, 0, 0, 0, 0, -1}};
 // x^(-1/q), q = 1..6: a linear start on m ∈ [0.5, 1), six Newton steps, the exponent part
 // 2^(−r/q)·2^(−Q) from a table (as inv_fifth_root)
 __device__ const double kIrS[7] = {0.0, -2.0, -0.8284271247461903, -0.5198420997897464, -0.37841423000544205,
@@ -95,395 +79,546 @@ __device__ __forceinline__ double norm_max(double c, const double (&v)[S], const
   if (!__builtin_isfinite(el) || __builtin_isnan(nfe)) el = 1e30;
   return el;
 }
+}  // namespace bdf
+}  // namespace oe
 
-// scipy's change_D for a step-size change by `factor` at order q, in two stages:
-// E = R(q, factor)^T D, then D = U^T E (the same product as (RU)^T D, U exact).  The R
-// coefficients r[m][i] = R[i][m] once (wave-uniform), then state by state, so only one
-// state's E is live.
-template <int S>
-__device__ __forceinline__ void change_D(double (&D)[kRows][S], int q, double factor) {
-  const cptr<double> U = kconst(&kU[0][0]), inv_i = kconst(kInvI);
-  double r[kMaxQ + 1][kMaxQ + 1];
+// ---- The pass: one step size and one order per lane (every kernel with S <= 8) ----------
+// In the reference every walker is integrated by its own odeint call (Framework.py:656, one
+// chain per process at :779-780), so nothing a walker computes depends on the others.  (Until
+// round 4 the lanes handed to BDF shared h and q over the wave, which made an MH chain's
+// bits depend on which proposals shared its wave: the speculation depth, the rank count.)
+// Every decision is the lane's own — HINIT without a wave minimum, the error norm without a
+// wave maximum, its own Newton outcome, order selection and budget — so a lane's result is
+// bdf_group of oracle/rk_ref.c on a group of one, operation for operation.  Against the
+// shared-step pass it also costs 20-30 % less per step on a lone stiff lane
+// (tools/bdf_cost.py, profiles/NOTES.md round 5).
+//
+// Layout of a step (one attempt per live lane per loop trip, lanes diverge freely):
+//   A  predictor (order-dependent: a switch on the lane's q, each case straight-line code
+//      for a compile-time order, so lanes at one order run it once);
+//   B  factors of I − c·J if needed and the modified Newton iteration (order-independent:
+//      every live lane together, whatever its order);
+//   C  the error test, the difference update, the grid points and the order selection
+//      (again a switch on q).
+// A Newton failure on factors from an earlier step retries the same attempt on the next
+// trip with factors at the predictor (the predictor is recomputed from unchanged inputs:
+// the same bits), as scipy's BDF and the group restatement do within one attempt.
+//
+// Registers (the MH kernels sit at one wave per SIMD): the Jacobian is taken column by
+// column with one-tangent dual numbers straight into the LU array (an S + 1-tangent
+// evaluation, stiff.cuh jac_eval, holds S² + S·(S + 2) doubles at once), the difference table
+// holds rows 0..q+1 plus the order-up row, i.e. kMaxQ + 2 rows (row kMaxQ + 2 is never read),
+// in LDS (below), and grid times come through a 4-entry window.
+//
+// Observations are deferred: at an observed grid point the lane only forms each record's
+// sum C (and tracks the minimum and finiteness), storing C to a per-lane column of the
+// launch's scratch (DevProblem::obs_c, [n_obs][lanes]); after the pass the wave adds the
+// chi / R² terms of every lane's records in record order, in uniform control flow — the
+// same terms in the same order as an immediate evaluation, and the out-of-line log is
+// never called under a partial EXEC mask.
+
+namespace oe {
+namespace bdfl {
+constexpr int kMaxQ = bdf::kMaxQ;
+constexpr int kRows = kMaxQ + 2;  // D[0..kMaxQ+1]; D[q+2] only while q < kMaxQ
+constexpr int kWin = 4;           // grid-time window (times[] carries kGridWin + 1 >= kWin sentinels)
+static_assert(kWin <= kGridWin + 1, "grid window past the sentinels");
+
+// bdf.cuh's tables as compile-time functions: with a template order they fold to immediates
+__device__ __forceinline__ constexpr double gam(int j) {
+  return j == 1 ? 1.0 : j == 2 ? 1.5 : j == 3 ? 1.8333333333333333 : j == 4 ? 2.083333333333333 : 2.283333333333333;
+}
+__device__ __forceinline__ constexpr double ialpha(int q) {
+  return q == 1 ? 0.8438818565400843 : q == 2 ? 0.6 : q == 3 ? 0.5039772202296456 : q == 4 ? 0.4608737397983678
+                                                                                             : 0.43795620437956206;
+}
+__device__ __forceinline__ constexpr double ec(int q) {
+  return q == 0 ? 1.0 : q == 1 ? 0.315 : q == 2 ? 0.16666666666666666 : q == 3 ? 0.09911666666666669
+         : q == 4 ? 0.11354166666666668 : 0.16666666666666666;
+}
+__device__ __forceinline__ constexpr double inv_i(int i) {
+  return i == 1 ? 1.0 : i == 2 ? 0.5 : i == 3 ? 0.3333333333333333 : i == 4 ? 0.25 : 0.2;
+}
+// U[m][j] = (−1)^m·C(j, m)
+__device__ __forceinline__ constexpr double U(int m, int j) {
+  double c = 1.0;
+  for (int k = 0; k < m; ++k) c = c * (double)(j - k) / (double)(k + 1);
+  return (m & 1) ? -c : c;
+}
+// x^(-1/q) start and scale tables (bdf.cuh kIrS / kIrI / kIrRq / kIrC)
+__device__ __forceinline__ constexpr double ir_s(int q) {
+  return q == 1 ? -2.0 : q == 2 ? -0.8284271247461903 : q == 3 ? -0.5198420997897464 : q == 4 ? -0.37841423000544205
+         : q == 5 ? -0.2973967099940702 : -0.24492409661874603;
+}
+__device__ __forceinline__ constexpr double ir_i(int q) {
+  return q == 1 ? 3.0 : q == 2 ? 1.8284271247461903 : q == 3 ? 1.5198420997897464 : q == 4 ? 1.378414230005442
+         : q == 5 ? 1.2973967099940702 : 1.244924096618746;
+}
+__device__ __forceinline__ constexpr double ir_rq(int q) {
+  return q == 1 ? 1.0 : q == 2 ? 0.5 : q == 3 ? 0.3333333333333333 : q == 4 ? 0.25 : q == 5 ? 0.2 : 0.16666666666666666;
+}
+template <int Q>
+__device__ __forceinline__ double ir_c(int r) {
+  static_assert(Q >= 1 && Q <= 6, "order");
+  if constexpr (Q == 1) return 1.0;
+  if constexpr (Q == 2) return r == 0 ? 1.0 : 0.7071067811865476;
+  if constexpr (Q == 3) return r == 0 ? 1.0 : r == 1 ? 0.7937005259840998 : 0.6299605249474366;
+  if constexpr (Q == 4) return r == 0 ? 1.0 : r == 1 ? 0.8408964152537145 : r == 2 ? 0.7071067811865476 : 0.5946035575013605;
+  if constexpr (Q == 5)
+    return r == 0 ? 1.0 : r == 1 ? 0.8705505632961241 : r == 2 ? 0.757858283255199 : r == 3 ? 0.6597539553864471
+                                                                                    : 0.5743491774985174;
+  if constexpr (Q == 6)
+    return r == 0 ? 1.0 : r == 1 ? 0.8908987181403393 : r == 2 ? 0.7937005259840998 : r == 3 ? 0.7071067811865476
+           : r == 4 ? 0.6299605249474366 : 0.5612310241546865;
+}
+// bdf::inv_root for a compile-time q: the same operations (constant division, unrolled
+// powers), the same bits
+template <int Q>
+__device__ __forceinline__ double inv_root(double x) {
+  if (!(x > 0.0)) return __builtin_inf();
+  if (__builtin_isinf(x)) return 0.0;
+  int e;
+  const double m = frexp(x, &e);
+  int E = e / Q, r = e % Q;
+  if (r < 0) { r += Q; E -= 1; }
+  double y = fma(ir_s(Q), m, ir_i(Q));
+  constexpr double q1 = (double)(Q + 1), rqq = ir_rq(Q);
 #pragma unroll
-  for (int m = 1; m <= kMaxQ; ++m) {
-    if (m > q) break;
+  for (int it = 0; it < 6; ++it) {
+    double yq = y;
+#pragma unroll
+    for (int j = 1; j < Q; ++j) yq = yq * y;
+    y = (y * fma(-m, yq, q1)) * rqq;
+  }
+  return ldexp(ir_c<Q>(r) * y, -E);
+}
+// Newton-count safety 0.9·(2·4 + 1)/(2·4 + n), n = 1..4
+__device__ __forceinline__ double safety(int n) {
+  return n == 1 ? 0.8999999999999999 : n == 2 ? 0.8099999999999999 : n == 3 ? 0.7363636363636363 : 0.6749999999999999;
+}
+}  // namespace bdfl
+
+// A lane's difference table lives in LDS, lane-minor ([row·S + s][kMhBlock] doubles, a
+// 512-B row per wave access): in registers, an update of the table inside the per-lane
+// switch on the order keeps two copies of it live (the new rows of the lanes in one case
+// while the next case runs on the old rows) — 28 doubles more at S = 4, which pushed the
+// kernel past 256 VGPRs.  In LDS the lanes' stores are masked writes in place.
+constexpr int kMhBlock = 256;  // threads per workgroup of every kernel with a BDF pass (capi.hip kBlock)
+#ifndef OE_BDF_D_REGS  // measurement builds: the difference table in registers (tools/build_alt.sh)
+#define OE_BDF_D_REGS 0
+#endif
+template <int S>
+struct DTab {
+#if OE_BDF_D_REGS
+  double v[bdfl::kRows * S];
+  __device__ __forceinline__ double& operator()(int r, int s) { return v[r * S + s]; }
+  __device__ __forceinline__ double operator()(int r, int s) const { return v[r * S + s]; }
+#else
+  double* p;  // this lane's column (LDS: the address space is inferred after inlining)
+  __device__ __forceinline__ double& operator()(int r, int s) const { return p[(r * S + s) * kMhBlock]; }
+#endif
+};
+template <int S>
+__device__ __forceinline__ DTab<S> dtab_column() {
+#if OE_BDF_D_REGS
+  return DTab<S>{};
+#else
+  __shared__ double tab[bdfl::kRows * S * kMhBlock];
+  return DTab<S>{tab + threadIdx.x};
+#endif
+}
+
+template <int S>
+struct BdfLane {
+  DTab<S> D;                 // backward differences (scipy's D), in LDS
+  double lu[S][S], dinv[S];  // LU of I − c·J
+  int piv[S];
+  double t, h;               // this lane's time and step size
+  double wv[bdfl::kWin];     // times[i .. i + kWin)
+  int q, neq, nst;           // order, steps at this h and q, steps since the last grid point
+  int i, k, nxt;             // next grid index, next observation record, its grid index
+  bool live, lu_ok, fresh, refac, swp;
+};
+
+// scipy's change_D at a compile-time order Q (bdf::change_D's operations)
+template <int S, int Q>
+__device__ __forceinline__ void bdfl_change_D(DTab<S>& D, double factor) {
+  using namespace bdfl;
+  double r[Q + 1][Q + 1];
+#pragma unroll
+  for (int m = 1; m <= Q; ++m) {
     double v = 1.0;
 #pragma unroll
-    for (int i = 1; i <= kMaxQ; ++i) {
-      if (i > q) break;
-      v = v * (((double)(i - 1) - factor * (double)m) * inv_i[i]);
+    for (int i = 1; i <= Q; ++i) {
+      v = v * (((double)(i - 1) - factor * (double)m) * inv_i(i));
       r[m][i] = v;
     }
   }
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    double E[kMaxQ + 1];
-    E[0] = D[0][s];
+    double E[Q + 1];
+    E[0] = D(0, s);
 #pragma unroll
-    for (int m = 1; m <= kMaxQ; ++m) {
-      if (m > q) break;
-      double e = D[0][s];
+    for (int m = 1; m <= Q; ++m) {
+      double e = D(0, s);
 #pragma unroll
-      for (int i = 1; i <= kMaxQ; ++i) {
-        if (i > q) break;
-        e = fma(r[m][i], D[i][s], e);
-      }
+      for (int i = 1; i <= Q; ++i) e = fma(r[m][i], D(i, s), e);
       E[m] = e;
     }
 #pragma unroll
-    for (int j = 0; j <= kMaxQ; ++j) {
-      if (j > q) break;
+    for (int j = 0; j <= Q; ++j) {
       double acc = E[0];
 #pragma unroll
-      for (int m = 1; m <= kMaxQ; ++m) {
-        if (m > j) break;
-        acc = fma(U[m * 6 + j], E[m], acc);
-      }
-      D[j][s] = acc;
+      for (int m = 1; m <= j; ++m) acc = fma(U(m, j), E[m], acc);
+      D(j, s) = acc;
     }
   }
 }
 
-// row `j` (wave-uniform, runtime) of D without indexing the register array
 template <int S>
-__device__ __forceinline__ void row(const double (&D)[kRows][S], int j, double (&out)[S]) {
-#pragma unroll
-  for (int s = 0; s < S; ++s) out[s] = 0.0;
-#pragma unroll
-  for (int r = 0; r < kRows; ++r)
-    if (r == j) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) out[s] = D[r][s];
-    }
+__device__ __forceinline__ void bdfl_change_D(DTab<S>& D, int q, double factor) {
+  switch (q) {
+    case 1: bdfl_change_D<S, 1>(D, factor); break;
+    case 2: bdfl_change_D<S, 2>(D, factor); break;
+    case 3: bdfl_change_D<S, 3>(D, factor); break;
+    case 4: bdfl_change_D<S, 4>(D, factor); break;
+    default: bdfl_change_D<S, 5>(D, factor); break;
+  }
 }
-}  // namespace bdf
 
-// the observations at grid index i (the lane's next observed one): fused chi / R² terms, and
-// the next observed index
+// Phase A: predictor y_p = Σ_{j<=Q} D_j, ψ = Σ γ_j D_j / α_Q, c = h / α_Q
+template <int S, int Q>
+__device__ __forceinline__ void bdfl_predict(const BdfLane<S>& st, double (&yp)[S], double (&psi)[S], double& c) {
+  using namespace bdfl;
+  constexpr double ia = ialpha(Q);
+  c = st.h * ia;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    double v = st.D(0, s), ps = 0.0;
+#pragma unroll
+    for (int j = 1; j <= Q; ++j) {
+      v = v + st.D(j, s);
+      ps = fma(gam(j), st.D(j, s), ps);
+    }
+    yp[s] = v;
+    psi[s] = ps * ia;
+  }
+}
+
+// LU factors of I − c·J(t, y): J column by column (one-tangent duals; each entry the same
+// bits as the S + 1-tangent evaluation), straight into the LU array
+template <class M, int PMAX>
+__device__ __forceinline__ void bdfl_factor(BdfLane<M::S>& st, double c, const double (&y)[M::S], double t,
+                                            const double (&p)[PMAX]) {
+  constexpr int S = M::S;
+  using D1 = Dual<1>;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    D1 yd[S], pd[PMAX], fd[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) { yd[s] = D1(y[s]); yd[s].d[0] = (s == j) ? 1.0 : 0.0; }
+    const D1 td(t);
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) pd[q] = D1(p[q]);
+    M::rhs(yd, td, pd, fd);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double av = c * fd[s].d[0];
+      st.lu[s][j] = (s == j) ? 1.0 - av : -av;
+    }
+  }
+  st.swp = ros::lu_factor<S>(st.lu, st.piv, st.dinv);
+}
+
+// the launch's deferred-observation scratch: record k of lane `col` at obs_c[k·ld + col]
+struct ObsCol {
+  double* c;
+  int64_t ld, col;
+};
+// TRAJ: this lane's column of the [T][S][W] trajectory
+struct TrajCol {
+  double* traj;
+  int64_t W, w;
+  bool active;
+};
+
+// the observations at grid index nxt (the lane's next observed one): finiteness, and each
+// record's sum C to the scratch (the chi / R² terms follow after the pass)
 template <int S>
-__device__ __forceinline__ void observe_lane(const DevProblem& pb, int i, const double (&y)[S], int& k, int& nxt,
+__device__ __forceinline__ void bdfl_observe(const DevProblem& pb, BdfLane<S>& st, const double (&yo)[S], const ObsCol& oc,
                                              Acc& a) {
+  check_finite(yo, a);
   const Obs* obs = pb.obs;
-  check_finite(y, a);
+  const int i = st.nxt;
+  int k = st.k;
   while (k < pb.n_obs && obs[k].tidx == i) {
     const uint64_t mask = obs[k].mask;
-    const double O = obs[k].O, two_s2 = obs[k].two_s2, O_lin = obs[k].O_lin;
     double c = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s)
-      if ((mask >> s) & 1ull) c = c + y[s];
-    const double d = O - oe_log(c);
-    const double term = (d * d) / two_s2;
-    if (__builtin_isfinite(term)) { a.chi += term; a.nvalid += 1; }
-    const double r = c - O_lin;
-    const double r2 = r * r;
-    if (!__builtin_isnan(r2)) a.ssres += r2;
+      if ((mask >> s) & 1ull) c = c + yo[s];
+    oc.c[(int64_t)k * oc.ld + oc.col] = c;
     ++k;
   }
-  nxt = (k < pb.n_obs) ? obs[k].tidx : 0x7fffffff;
+  st.k = k;
+  st.nxt = (k < pb.n_obs) ? obs[k].tidx : 0x7fffffff;
 }
 
-// Output of one lane at its own grid index i (trajectory row store + minimum + observations):
-// per-lane addresses, so plain stores/loads instead of the uniform buffer descriptors.
-// Without a trajectory only observed grid points are emitted (as the DOPRI5 pass does).
-// `nxt` is the lane's next observed grid index, carried in a register: an unobserved row does
-// no load.  The row stores come last: on gfx950 a vector load's wait also waits for every
-// store issued before it, so a load after the stores (the old obs[k] test) held each row
-// until its stores had completed (C2-stiffmix `auto`: ~2.3 us per BDF row).
-template <int S, bool TRAJ, bool NT>
-__device__ __forceinline__ void emit_lane(const DevProblem& pb, int i, const double (&y)[S], double* traj, int64_t W,
-                                          int64_t w, bool active, int& k, int& nxt, Acc& a) {
-  const bool observed = i == nxt;
-  if (!TRAJ && !observed) return;
-  track_min<S>(y, a);
-  if (observed) observe_lane<S>(pb, i, y, k, nxt, a);
-  if constexpr (TRAJ) {
-    if (active) {
-      double* row = traj + (int64_t)i * S * W + w;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if constexpr (NT) __builtin_nontemporal_store(y[s], row + (int64_t)s * W);
-        else row[(int64_t)s * W] = y[s];
-      }
-    }
-  }
-}
-
-// The per-lane state of the BDF pass and the wave-shared controls.
-template <int S>
-struct BdfState {
-  double D[bdf::kRows][S];  // backward differences (scipy's D)
-  double lu[S][S], dinv[S]; // LU of I − c·J (J evaluated when the factors are built)
-  int piv[S];
-  double t;                 // this lane's time
-  double ti;                // times[i] (times[T] is the +inf sentinel), loaded ahead
-  int i, k, nst;            // next grid index, next observation, steps since the last grid point
-  int nxt;                  // grid index of observation k (INT_MAX past the last)
-  bool live;
-  // wave-uniform
-  double h;
-  int order, neq;
-  bool lu_ok, fresh, any_swap;  // factors valid; built in this step (from this step's Jacobian)
-};
-
-// LU factors of I − c·J(t, y) for the lanes taking part
-template <class M, int PMAX>
-__device__ __forceinline__ void bdf_factor(BdfState<M::S>& st, double c, const double (&y)[M::S], double t,
-                                           const double (&p)[PMAX]) {
-  constexpr int S = M::S;
-  double f[S], ft[S];
-  jac_eval<M, PMAX>(y, t, p, f, st.lu, ft);
-#pragma unroll
-  for (int r = 0; r < S; ++r)
-#pragma unroll
-    for (int q = 0; q < S; ++q) {
-      const double av = c * st.lu[r][q];
-      st.lu[r][q] = (r == q) ? 1.0 - av : -av;
-    }
-  st.any_swap = ros::lu_factor<S>(st.lu, st.piv, st.dinv);
-}
-
-// What an accepted step hands to the (order-generic) output and order selection.
-struct BdfAccepted {
-  double h, en, safety;  // the step size used, the wave error norm, the Newton-count safety
-  double em_l, ep_l;     // this lane's norms at orders q − 1 and q + 1 (select steps)
-  bool select;           // wave-uniform: order and step selection after this step
-};
-
-// One step attempt at order Q (compile-time, so the difference rows are fixed registers and
-// the loops over them are straight-line code).  Returns false on a rejected attempt (h and D
-// already rescaled for the retry); on acceptance the lanes' differences are updated and the
-// grid output and order selection follow in bdf_output / bdf_select (order-generic: written
-// once rather than once per order).
-template <class M, int PMAX, int Q>
-__device__ __forceinline__ bool bdf_attempt(const DevProblem& pb, BdfState<M::S>& st, const double (&p)[PMAX],
-                                            BdfAccepted& acc) {
-  using namespace bdf;
-  constexpr int S = M::S;
-  const double rtol = pb.rtol, atol = pb.atol, ntol = pb.newton_tol;
-  const cptr<double> gam = kconst(kGamma);
-  const double ialpha = kconst(kInvAlpha)[Q];
+// the backward-difference interpolant of the step just accepted (order Q, ending at tn) at ti
+template <int S, int Q>
+__device__ __forceinline__ void bdfl_interp(const BdfLane<S>& st, double tn, double ti, double (&yo)[S]) {
   const double h = st.h;
-  const double c = h * ialpha;
-  double yp[S], psi[S], rs[S];
+  double prod = 1.0;
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    double v = st.D[0][s], ps = 0.0;
+  for (int s = 0; s < S; ++s) yo[s] = st.D(0, s);
 #pragma unroll
-    for (int j = 1; j <= Q; ++j) {
-      v = v + st.D[j][s];
-      ps = fma(gam[j], st.D[j][s], ps);
-    }
-    yp[s] = v;
-    psi[s] = ps * ialpha;
-    rs[s] = 1.0 / fma(rtol, fabs(v), atol);
+  for (int j = 1; j <= Q; ++j) {
+    const double rden = 1.0 / ((double)j * h);
+    const double x = (ti - (tn - (double)(j - 1) * h)) * rden;
+    prod = prod * x;
+#pragma unroll
+    for (int s = 0; s < S; ++s) yo[s] = fma(st.D(j, s), prod, yo[s]);
   }
-  double yn[S], d[S];
-  bool bad = false;
-  int niter = 0;
-  if (!st.lu_ok) {  // factors for this step size and order, Jacobian at the current state
-    double y0[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) y0[s] = st.D[0][s];
-    bdf_factor<M, PMAX>(st, c, y0, st.t, p);
-    st.lu_ok = true;
-    st.fresh = true;
-  }
-  for (;;) {  // Newton; once more on factors from this step's predictor if it fails on older ones
-#pragma unroll
-    for (int s = 0; s < S; ++s) { yn[s] = yp[s]; d[s] = 0.0; }
-    bool conv = false, fail = false;
-    double dold = 0.0;
-    niter = 0;
-    for (int kk = 0; kk < kNewtonMaxIter; ++kk) {
-      const bool act = st.live && !conv && !fail;
-      if (__ballot(act) == 0ull) break;
-      niter = kk + 1;
-      if (act) {
-        double f[S], dy[S], nf = 0.0;
-        M::rhs(yn, st.t + h, p, f);
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          nf = fma(f[s], 0.0, nf);
-          dy[s] = (c * f[s] - psi[s]) - d[s];
-        }
-        if (__builtin_isnan(nf)) {
-          fail = true;
-        } else {
-          ros::lu_solve<S>(st.lu, st.piv, st.dinv, st.any_swap, dy);
-          double dn = 0.0;
-#pragma unroll
-          for (int s = 0; s < S; ++s) dn = fmax(dn, fabs(dy[s]) * rs[s]);
-          double rate = 0.0;
-          bool ok = true;
-          if (kk > 0) {
-            rate = dn / dold;
-            const double pw = (kk == 1) ? (rate * rate) * rate : (kk == 2) ? rate * rate : rate;
-            if (!(rate < 1.0) || pw / (1.0 - rate) * dn > ntol) { fail = true; ok = false; }
-          }
-          if (ok) {
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-              yn[s] = yn[s] + dy[s];
-              d[s] = d[s] + dy[s];
-            }
-            if (dn == 0.0 || (kk > 0 && rate / (1.0 - rate) * dn < ntol)) conv = true;
-            dold = dn;
-          }
-        }
-      }
-    }
-    bad = __ballot(st.live && !conv) != 0ull;
-    if (!bad || st.fresh) break;
-    bdf_factor<M, PMAX>(st, c, yp, st.t + h, p);
-    st.fresh = true;
-  }
-  if (bad) {
-    st.h = h * 0.5;
-    change_D<S>(st.D, Q, 0.5);
+}
+
+// Phase C at order Q: error test; on acceptance the differences, the grid points of
+// (t, t + h] and — every Q + 1 equal steps — the order and step selection
+template <class M, int Q, bool TRAJ, bool NT>
+__device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S>& st, const double (&yn)[M::S],
+                                              const double (&d)[M::S], int niter, double (&y)[M::S], const ObsCol& oc,
+                                              const TrajCol& tc, Acc& a) {
+  using namespace bdfl;
+  constexpr int S = M::S;
+  const double rtol = pb.rtol, atol = pb.atol;
+  const double sf = safety(niter);
+  const double el = bdf::norm_max<S>(ec(Q), d, yn, rtol, atol);
+  if (el > 1.0) {  // rejected on the error (the factors are kept, as scipy)
+    const double factor = fmax(0.2, sf * inv_root<Q + 1>(el));
+    st.h = st.h * factor;
+    bdfl_change_D<S, Q>(st.D, factor);
     st.neq = 0;
-    st.lu_ok = false;
-    return false;
+    return;
   }
-  const double safety = kconst(kSafety)[niter];
-  const cptr<double> ec = kconst(kEc);
-  const double el = st.live ? norm_max<S>(ec[Q], d, yn, rtol, atol) : 0.0;
-  const double en = wave_max(el);
-  if (en > 1.0) {
-    const double factor = fmax(0.2, safety * inv_root(en, Q + 1));
-    st.h = h * factor;
-    change_D<S>(st.D, Q, factor);
-    st.neq = 0;
-    return false;
-  }
-#ifdef OE_BDF_TRACE
-  if (st.live && blockIdx.x == 0 && threadIdx.x == 0) printf("ACC Q=%d t=%.17g h=%.17g niter=%d\n", Q, st.t, h, niter);
-#endif
   ++st.neq;
   st.fresh = false;
-  acc.h = h;
-  acc.en = en;
-  acc.safety = safety;
-  acc.select = st.neq >= Q + 1;
-  acc.em_l = 0.0;
-  acc.ep_l = 0.0;
-  if (st.live) {  // the differences of the accepted step
+  const double tn = st.t + st.h;
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      st.D[Q + 2][s] = d[s] - st.D[Q + 1][s];
-      st.D[Q + 1][s] = d[s];
-    }
-#pragma unroll
-    for (int j = Q; j >= 0; --j)
-#pragma unroll
-      for (int s = 0; s < S; ++s) st.D[j][s] = st.D[j][s] + st.D[j + 1][s];
-    if (acc.select) {  // the candidates' norms (used by the lanes still running after the output)
-      if constexpr (Q > 1) acc.em_l = norm_max<S>(ec[Q - 1], st.D[Q], yn, rtol, atol);
-      if constexpr (Q < kMaxQ) acc.ep_l = norm_max<S>(ec[Q + 1], st.D[Q + 2], yn, rtol, atol);
-    }
+  for (int s = 0; s < S; ++s) {
+    if constexpr (Q + 2 < kRows) st.D(Q + 2, s) = d[s] - st.D(Q + 1, s);
+    st.D(Q + 1, s) = d[s];
   }
-  return true;
-}
-
-// The grid points of an accepted step of order q (wave-uniform, runtime) from the
-// backward-difference interpolant; a lane past its last grid point leaves (y = that row).
-template <int S, bool TRAJ, bool NT>
-__device__ __forceinline__ void bdf_output(const DevProblem& pb, BdfState<S>& st, int q, double h, double (&y)[S],
-                                           double* traj, int64_t W, int64_t w, bool active, Acc& a) {
-  using namespace bdf;
-  if (!st.live) return;
-  const double tn = st.t + h;
+#pragma unroll
+  for (int j = Q; j >= 0; --j)
+#pragma unroll
+    for (int s = 0; s < S; ++s) st.D(j, s) = st.D(j, s) + st.D(j + 1, s);
   ++st.nst;
-  double yo[S];
-  const double* times = pb.times;
-  double rden[kMaxQ + 1];  // 1/(j·h): one division per order per step, not per grid point
+  // grid points in (t, tn]: counted on the window, a window's worth at a time; the rows
+  // (TRAJ), the observed points and T − 1 (the final state) from the interpolant
+  int i = st.i, c;
+  bool crossed = false;
+  do {
+    c = 0;
 #pragma unroll
-  for (int j = 1; j <= kMaxQ; ++j) {
-    if (j > q) break;
-    rden[j] = 1.0 / ((double)j * h);
-  }
-  while (st.ti <= tn) {  // (st.i < T: times[T] is +inf)
-    const double ti = st.ti;
-    const int i = st.i;
-    st.i = i + 1;
-    const double tnext = times[st.i];  // in flight while this row is formed and stored
-    if (TRAJ || i == st.nxt || i == pb.T - 1) {  // without a trajectory: observed rows, the final state
-      double prod = 1.0;
+    for (int j = 0; j < kWin; ++j) c += (st.wv[j] <= tn) ? 1 : 0;
+    if (c == 0) break;
+    crossed = true;
+    for (int j = 0; j < c; ++j) {
+      const int g = i + j;
+      const bool observed = g == st.nxt;
+      if (TRAJ || observed || g == pb.T - 1) {
+        double yo[S];
+        bdfl_interp<S, Q>(st, tn, pick(st.wv, j), yo);
+        if (TRAJ || observed) track_min<S>(yo, a);
+        if constexpr (TRAJ) {
+          if (tc.active) {
+            double* row = tc.traj + (int64_t)g * S * tc.W + tc.w;
 #pragma unroll
-      for (int s = 0; s < S; ++s) yo[s] = st.D[0][s];
+            for (int s = 0; s < S; ++s) {
+              if constexpr (NT) __builtin_nontemporal_store(yo[s], row + (int64_t)s * tc.W);
+              else row[(int64_t)s * tc.W] = yo[s];
+            }
+          }
+        }
+        if (observed) bdfl_observe<S>(pb, st, yo, oc, a);
+        if (g == pb.T - 1) {
 #pragma unroll
-      for (int j = 1; j <= kMaxQ; ++j) {
-        if (j > q) break;
-        const double x = (ti - (tn - (double)(j - 1) * h)) * rden[j];
-        prod = prod * x;
-#pragma unroll
-        for (int s = 0; s < S; ++s) yo[s] = fma(st.D[j][s], prod, yo[s]);
+          for (int s = 0; s < S; ++s) y[s] = yo[s];
+        }
       }
-#ifdef OE_BDF_TRACE
-      if (blockIdx.x == 0 && threadIdx.x == 0) printf("EMIT i=%d y1=%.17g\n", i, yo[1]);
-#endif
-      emit_lane<S, TRAJ, NT>(pb, i, yo, traj, W, w, active, st.k, st.nxt, a);
     }
-    st.ti = tnext;
+    i += c;
+#pragma unroll
+    for (int j = 0; j < kWin; ++j) st.wv[j] = pb.times[i + j];  // (times[T..] are +inf sentinels)
+  } while (c == kWin);
+  if (crossed) {
     st.nst = 0;
+    st.i = i;
+    if (i >= pb.T) {  // past the last grid point: done (y holds its interpolant)
+      st.t = tn;
+      st.live = false;
+      return;
+    }
   }
   st.t = tn;
-  if (st.i >= pb.T) {
+  if (st.neq >= Q + 1) {  // order and step selection (scipy's rule, capped at 10)
+    double fm = 0.0, fp = 0.0;
+    if constexpr (Q > 1) {
+      double v[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) y[s] = yo[s];
-    st.live = false;
+      for (int s = 0; s < S; ++s) v[s] = st.D(Q, s);
+      fm = inv_root<Q>(bdf::norm_max<S>(ec(Q - 1), v, yn, rtol, atol));
+    }
+    const double fe = inv_root<Q + 1>(el);
+    if constexpr (Q < kMaxQ) {
+      double v[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) v[s] = st.D(Q + 2, s);
+      fp = inv_root<Q + 2>(bdf::norm_max<S>(ec(Q + 1), v, yn, rtol, atol));
+    }
+    int dq = 0;
+    double fmx = fm;
+    if (fe > fmx) { fmx = fe; dq = 1; }
+    if (fp > fmx) { fmx = fp; dq = 2; }
+    const double factor = fmin(10.0, sf * fmx);
+    st.h = st.h * factor;
+    if (dq == 0) {
+      if constexpr (Q > 1) bdfl_change_D<S, Q - 1>(st.D, factor);
+    } else if (dq == 1) {
+      bdfl_change_D<S, Q>(st.D, factor);
+    } else {
+      if constexpr (Q < kMaxQ) bdfl_change_D<S, Q + 1>(st.D, factor);
+    }
+    st.q = Q + dq - 1;
+    st.neq = 0;
+    st.lu_ok = false;
   }
 }
 
-// Order and step-size selection after an accepted select step of order q (scipy's rule:
-// the largest of the three factors, capped at 10), voted by the lanes still running.
-template <int S>
-__device__ __forceinline__ void bdf_select(BdfState<S>& st, int q, const BdfAccepted& acc) {
-  using namespace bdf;
-  const bool voter = st.live;
-  if (__ballot(voter) == 0ull) return;
-  const double em = wave_max(voter ? acc.em_l : 0.0), ep = wave_max(voter ? acc.ep_l : 0.0);
-  const double fm = (q > 1) ? inv_root(em, q) : 0.0;
-  const double fe = inv_root(acc.en, q + 1);
-  const double fp = (q < kMaxQ) ? inv_root(ep, q + 2) : 0.0;
-  int dq = 0;
-  double fmx = fm;
-  if (fe > fmx) { fmx = fe; dq = 1; }
-  if (fp > fmx) { fmx = fp; dq = 2; }
-  const int nq = q + dq - 1;
-  const double factor = fmin(10.0, acc.safety * fmx);
-  st.h = acc.h * factor;
-  change_D<S>(st.D, nq, factor);
-  st.order = nq;
-  st.neq = 0;
-  st.lu_ok = false;
+// One step attempt of a live lane (called in divergent control flow)
+template <class M, int PMAX, bool TRAJ, bool NT>
+__device__ __forceinline__ void bdfl_step(const DevProblem& pb, BdfLane<M::S>& st, const double (&p)[PMAX],
+                                          double (&y)[M::S], const ObsCol& oc, const TrajCol& tc, Acc& a) {
+  using namespace bdfl;
+  constexpr int S = M::S;
+  const double rtol = pb.rtol, atol = pb.atol, ntol = pb.newton_tol;
+  double yp[S], psi[S], c;
+  switch (st.q) {
+    case 1: bdfl_predict<S, 1>(st, yp, psi, c); break;
+    case 2: bdfl_predict<S, 2>(st, yp, psi, c); break;
+    case 3: bdfl_predict<S, 3>(st, yp, psi, c); break;
+    case 4: bdfl_predict<S, 4>(st, yp, psi, c); break;
+    default: bdfl_predict<S, 5>(st, yp, psi, c); break;
+  }
+  double rs[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) rs[s] = 1.0 / fma(rtol, fabs(yp[s]), atol);
+  if (!st.lu_ok || st.refac) {  // at the current state (new h or q), or at the predictor (retry)
+    double fy[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) fy[s] = st.refac ? yp[s] : st.D(0, s);
+    bdfl_factor<M, PMAX>(st, c, fy, st.refac ? st.t + st.h : st.t, p);
+    st.lu_ok = true;
+    st.fresh = true;
+    st.refac = false;
+  }
+  // ---- B: modified Newton (every live lane, whatever its order) ----
+  const double tn = st.t + st.h;
+  double yn[S], d[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) { yn[s] = yp[s]; d[s] = 0.0; }
+  bool conv = false, fail = false;
+  double dold = 0.0;
+  int niter = 0;
+  for (int kk = 0; kk < bdf::kNewtonMaxIter; ++kk) {
+    const bool act = !conv && !fail;
+    if (__ballot(act) == 0ull) break;
+    if (act) {
+      niter = kk + 1;
+      double f[S], dy[S], nf = 0.0;
+      M::rhs(yn, tn, p, f);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        nf = fma(f[s], 0.0, nf);
+        dy[s] = (c * f[s] - psi[s]) - d[s];
+      }
+      if (__builtin_isnan(nf)) {
+        fail = true;
+      } else {
+        ros::lu_solve<S>(st.lu, st.piv, st.dinv, st.swp, dy);
+        double dn = 0.0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) dn = fmax(dn, fabs(dy[s]) * rs[s]);
+        double rate = 0.0;
+        bool ok = true;
+        if (kk > 0) {
+          rate = dn / dold;
+          const double pw = (kk == 1) ? (rate * rate) * rate : (kk == 2) ? rate * rate : rate;
+          if (!(rate < 1.0) || pw / (1.0 - rate) * dn > ntol) { fail = true; ok = false; }
+        }
+        if (ok) {
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            yn[s] = yn[s] + dy[s];
+            d[s] = d[s] + dy[s];
+          }
+          if (dn == 0.0 || (kk > 0 && rate / (1.0 - rate) * dn < ntol)) conv = true;
+          dold = dn;
+        }
+      }
+    }
+  }
+  if (!conv) {
+    if (!st.fresh) {  // failed on older factors: this attempt again, on factors at the predictor
+      st.refac = true;
+      return;
+    }
+    st.h = st.h * 0.5;
+    bdfl_change_D<S>(st.D, st.q, 0.5);
+    st.neq = 0;
+    st.lu_ok = false;
+    return;
+  }
+  // ---- C ----
+  switch (st.q) {
+    case 1: bdfl_conclude<M, 1, TRAJ, NT>(pb, st, yn, d, niter, y, oc, tc, a); break;
+    case 2: bdfl_conclude<M, 2, TRAJ, NT>(pb, st, yn, d, niter, y, oc, tc, a); break;
+    case 3: bdfl_conclude<M, 3, TRAJ, NT>(pb, st, yn, d, niter, y, oc, tc, a); break;
+    case 4: bdfl_conclude<M, 4, TRAJ, NT>(pb, st, yn, d, niter, y, oc, tc, a); break;
+    default: bdfl_conclude<M, 5, TRAJ, NT>(pb, st, yn, d, niter, y, oc, tc, a); break;
+  }
 }
 
-// BDF integration of the lanes with `part` set from their own (t, y, grid index i,
-// observation index k) with their accumulators as they are; the others sit out (no vote,
-// no output).  y is the final state (the last grid point's) on return.
+// BDF integration, one step size and order per lane, of the lanes with `part` set from
+// their own (t, y, grid index i, observation record k); y is the final state on return.
+// W lanes in the launch, this lane's column w (the trajectory rows, TRAJ, and the scratch of
+// deferred observations).
 template <class M, int PMAX, bool TRAJ, bool NT>
-__device__ __forceinline__ void integrate_bdf(const DevProblem& pb, double (&y)[M::S], double t, int i, int k,
-                                              const double (&p)[PMAX], double* traj, int64_t W, int64_t w,
-                                              bool active, bool part, Acc& a) {
-  using namespace bdf;
+__device__ __forceinline__ void integrate_bdf_lane(const DevProblem& pb, double (&y)[M::S], double t, int i, int k,
+                                                   const double (&p)[PMAX], double* traj, int64_t W, int64_t w,
+                                                   bool active, bool part, Acc& a) {
+  using namespace bdfl;
   constexpr int S = M::S;
   const cptr<double> ctimes = kconst(pb.times);
   const double tend = ctimes[pb.T - 1], t0 = ctimes[0];
   const double rtol = pb.rtol, atol = pb.atol;
-  const int budget = kBudget * pb.max_steps;
-  BdfState<S> st;
+  const int budget = bdf::kBudget * pb.max_steps;
+  const ObsCol oc{pb.obs_c, W, w};
+  const TrajCol tc{traj, W, w, active};
+  const int k_first = k;
+  BdfLane<S> st;
+  st.D = dtab_column<S>();
   st.live = part;
   st.t = t;
   st.i = i;
   st.k = k;
-  st.ti = pb.times[i];
   st.nxt = (k < pb.n_obs) ? pb.obs[k].tidx : 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < kWin; ++j) st.wv[j] = pb.times[i + j];
   st.nst = 0;
   {
     double f[S];
     M::rhs(y, t, p, f);
-    // initial step: HINIT for order 1 (max norm), wave minimum over the lanes taking part
+    // initial step: HINIT for order 1 (max norm), this lane's own
     double d0 = 0.0, d1v = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -506,50 +641,63 @@ __device__ __forceinline__ void integrate_bdf(const DevProblem& pb, double (&y)[
     }
     d2 = d2 / h0;
     const double dm = fmax(d1v, d2);
-    const double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : inv_root(dm / 0.01, 2);
+    const double h1 = (dm <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : bdf::inv_root(dm / 0.01, 2);
     double hl = fmin(100.0 * h0, h1);
     if (!__builtin_isfinite(hl) || !(hl > 0.0)) hl = rest;
-    if (!st.live) hl = __builtin_inf();
-    st.h = wave_min(hl);
+    st.h = hl;
 #pragma unroll
     for (int j = 0; j < kRows; ++j)
 #pragma unroll
-      for (int s = 0; s < S; ++s) st.D[j][s] = 0.0;
+      for (int s = 0; s < S; ++s) st.D(j, s) = 0.0;
 #pragma unroll
-    for (int s = 0; s < S; ++s) { st.D[0][s] = y[s]; st.D[1][s] = f[s] * st.h; }
+    for (int s = 0; s < S; ++s) { st.D(0, s) = y[s]; st.D(1, s) = f[s] * st.h; }
   }
   const double hmin = 1e-14 * fmax(fabs(tend), fabs(t0)) + 1e-300;
-  st.order = 1;
+  st.q = 1;
   st.neq = 0;
   st.lu_ok = false;
   st.fresh = false;
-  st.any_swap = false;
+  st.refac = false;
+  st.swp = false;
   while (__ballot(st.live) != 0ull) {
-    const int q = st.order;  // wave-uniform
-    BdfAccepted acc;
-    bool ok;
-    switch (q) {
-      case 1: ok = bdf_attempt<M, PMAX, 1>(pb, st, p, acc); break;
-      case 2: ok = bdf_attempt<M, PMAX, 2>(pb, st, p, acc); break;
-      case 3: ok = bdf_attempt<M, PMAX, 3>(pb, st, p, acc); break;
-      case 4: ok = bdf_attempt<M, PMAX, 4>(pb, st, p, acc); break;
-      default: ok = bdf_attempt<M, PMAX, 5>(pb, st, p, acc); break;
-    }
-    if (ok) {
-      bdf_output<S, TRAJ, NT>(pb, st, q, acc.h, y, traj, W, w, active, a);
-      if (acc.select) bdf_select<S>(st, q, acc);
-    }
-    // budget: a lane that needs more than `budget` steps inside one output interval, or a
-    // step below hmin, is abandoned (MAXSTEP, NaN for the rest of its grid)
-    if (st.live && (st.nst >= budget || st.h < hmin)) {
-      st.live = false;
-      a.status |= ST_MAXSTEP;
-      double yo[S];
+    if (st.live) {
+      bdfl_step<M, PMAX, TRAJ, NT>(pb, st, p, y, oc, tc, a);
+      // budget: more than `budget` steps inside one output interval, or a step below hmin:
+      // abandoned (MAXSTEP; NaN at the later points — their records are not added)
+      if (st.live && (st.nst >= budget || st.h < hmin)) {
+        st.live = false;
+        a.status |= ST_MAXSTEP;
 #pragma unroll
-      for (int s = 0; s < S; ++s) yo[s] = __builtin_nan("");
-      for (; st.i < pb.T; ++st.i) emit_lane<S, TRAJ, NT>(pb, st.i, yo, traj, W, w, active, st.k, st.nxt, a);
+        for (int s = 0; s < S; ++s) y[s] = __builtin_nan("");
+        if constexpr (TRAJ) {  // NaN rows for the rest of the grid
+          if (active)
+            for (int g = st.i; g < pb.T; ++g) {
+              double* row = traj + (int64_t)g * S * W + w;
 #pragma unroll
-      for (int s = 0; s < S; ++s) y[s] = yo[s];
+              for (int s = 0; s < S; ++s) {
+                if constexpr (NT) __builtin_nontemporal_store(y[s], row + (int64_t)s * W);
+                else row[(int64_t)s * W] = y[s];
+              }
+            }
+        }
+      }
+    }
+  }
+  // deferred observations: records [k_first, st.k) of each taking-part lane, in record
+  // order, uniform control flow (every lane runs every record; the others drop it)
+  const double kmin = wave_min(part ? (double)k_first : __builtin_inf());
+  if (kmin < (double)pb.n_obs) {
+    const cptr<Obs> obs = kconst(pb.obs);
+    for (int kk = (int)kmin; kk < pb.n_obs; ++kk) {
+      const bool in = part && kk >= k_first && kk < st.k;
+      const double c = in ? oc.c[(int64_t)kk * oc.ld + oc.col] : 1.0;
+      const double O = obs[kk].O, two_s2 = obs[kk].two_s2, O_lin = obs[kk].O_lin;
+      const double dd = O - oe_log(c);
+      const double term = (dd * dd) / two_s2;
+      if (in && __builtin_isfinite(term)) { a.chi += term; a.nvalid += 1; }
+      const double r = c - O_lin;
+      const double r2 = r * r;
+      if (in && !__builtin_isnan(r2)) a.ssres += r2;
     }
   }
   if (part) check_finite(y, a);

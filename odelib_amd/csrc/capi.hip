@@ -106,7 +106,7 @@ struct oe_ctx {
   void* tree = nullptr;          // speculative MH rounds: node proposals and results
   size_t tree_bytes = 0;
   void* obs_buf = nullptr;       // MH 'auto' / 'bdf' (S <= 8): the per-lane BDF pass's deferred
-  size_t obs_bytes = 0;          // observations, [n_obs][lanes] (DevProblem::obs_c, bdf_lane.cuh)
+  size_t obs_bytes = 0;          // observations, [n_obs][lanes] (DevProblem::obs_c, bdf.cuh)
   int32_t last_mh_depth = 0;     // iterations per round of the last oe_mh_run (0: sequential)
   // OE_TUNE: the RK4 trajectory kernel chosen per shape, with what was measured (built-in
   // models: in a process-wide table shared by every context on the device; hipRTC models here)
@@ -877,6 +877,14 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     ia.y0 = d_y0; ia.theta = d_th; ia.traj = d_traj; ia.chi = d_chi; ia.ssres = d_ss; ia.status = d_st;
   } else {
     ia.y0 = y0; ia.theta = theta; ia.traj = traj; ia.chi = chi; ia.ssres = ssres; ia.status = status;
+  }
+  // the BDF pass ('auto' hand-over, 'bdf'; S <= 8) defers its observations to a
+  // [n_obs][W] scratch (bdf.cuh)
+  c->dp.obs_c = nullptr;
+  if ((c->method == OE_METHOD_AUTO || c->method == OE_METHOD_BDF) && S <= 8 && c->dp.n_obs > 0) {
+    rc = ensure_obs_buf(c, sizeof(double) * (size_t)c->dp.n_obs * (size_t)W);
+    if (rc) return rc;
+    c->dp.obs_c = static_cast<double*>(c->obs_buf);
   }
 
   // RK4 trajectories: one of the bitwise-identical kernels (OE_KERNEL_*).

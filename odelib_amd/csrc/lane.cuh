@@ -285,7 +285,8 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
   if constexpr (AUTO) {
     if (__ballot(handed) != 0ull) {  // wave-uniform: the BDF pass from each handed lane's (t, y, i, k)
       if (handed) a.status |= ST_STIFF;
-      integrate_bdf_lane<M, PMAX>(pb, y, t, i, k_lane, p, W, (int64_t)(off >> 3), handed, a);
+      integrate_bdf_lane<M, PMAX, false, false>(pb, y, t, i, k_lane, p, nullptr, W, (int64_t)(off >> 3), active,
+                                                handed, a);
     }
   }
 }

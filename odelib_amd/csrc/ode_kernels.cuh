@@ -55,7 +55,7 @@ struct DevProblem {
   double sstot;         // R² denominator
   double newton_tol;    // BDF Newton tolerance, max(10·eps/rtol, min(0.03, sqrt(rtol))) (host-computed)
   double* obs_c;        // MH launches: [n_obs][lanes] scratch of the per-lane BDF pass's deferred
-                        // observations (bdf_lane.cuh); null elsewhere
+                        // observations (bdf.cuh); null elsewhere
 };
 
 enum : int32_t { ST_NONFINITE = 1, ST_NEGATIVE = 2, ST_MAXSTEP = 4, ST_STIFF = 8, ST_INTERNAL = 16 };
@@ -936,12 +936,11 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
 }
 
 }  // namespace oe
-#include "stiff.cuh"
-#include "bdf.cuh"
 namespace oe {
 constexpr int kGridWin = 8;  // the time grid buffer carries kGridWin + 1 +inf sentinels (lane.cuh)
 }
-#include "bdf_lane.cuh"
+#include "stiff.cuh"
+#include "bdf.cuh"
 #include "lane.cuh"
 namespace oe {
 
@@ -968,15 +967,11 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
     integrate_dopri5_lane<M, PMAX, false>(pb, y, p, W, off, active, a);
   } else if constexpr (METHOD == kDOPRI5 || M::S > kStiffMaxS) {
     integrate_dopri5<M, PMAX, TRAJ, NT>(pb, y, p, traj, W, off, active, a);
-  } else if constexpr (LANE && METHOD == kBdf) {  // MH kernels: BDF from t0, own h and q per lane
-    int k = 0;
-    emit<M::S, false, false>(pb, 0, y, nullptr, W, off, active, k, a);
-    integrate_bdf_lane<M, PMAX>(pb, y, kconst(pb.times)[0], 1, k, p, W, w, active, a);
   } else if constexpr (METHOD == kBdf) {  // LSODA's BDF branch for every walker (S <= kStiffRegS)
     static_assert(M::S <= kStiffRegS, "bdf: register path only");
     int k = 0;
     emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
-    integrate_bdf<M, PMAX, TRAJ, NT>(pb, y, kconst(pb.times)[0], 1, k, p, traj, W, w, active, active, a);
+    integrate_bdf_lane<M, PMAX, TRAJ, NT>(pb, y, kconst(pb.times)[0], 1, k, p, traj, W, w, active, active, a);
   } else if constexpr (METHOD == kAuto && M::S <= kStiffRegS && LANE) {
     // per-lane DOPRI5 whose flagged lanes continue with BDF from their own eviction points
     // (the BDF pass is lane.cuh's tail: it starts from the DOPRI5 pass's live state)
@@ -997,7 +992,7 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
         a = rs.a;
         a.status |= ST_STIFF;
       }
-      integrate_bdf<M, PMAX, TRAJ, NT>(pb, rs.y, rs.t, rs.i, rs.k, p, traj, W, w, active, handed, a);
+      integrate_bdf_lane<M, PMAX, TRAJ, NT>(pb, rs.y, rs.t, rs.i, rs.k, p, traj, W, w, active, handed, a);
       if (handed) {
 #pragma unroll
         for (int s = 0; s < M::S; ++s) y[s] = rs.y[s];

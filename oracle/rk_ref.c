@@ -69,9 +69,10 @@ typedef struct {
   int split;     /* DOPRI5 with a walker over `split` lanes (odelib_amd/csrc/split.cuh): groups of
                     64/split walkers share a step size; a walker's error norm is the argmax over
                     each lane's states, combined in a tree of lanes (lower lane kept on ties) */
-  int lane_steps; /* DOPRI5 / 'auto' / 'bdf' without a trajectory, S <= 8 (odelib_amd/csrc/lane.cuh and
-                     bdf_lane.cuh, the MH kernels): every walker takes its own step sizes and BDF
-                     orders, i.e. the lockstep algorithms on a group of one */
+  int lane_steps; /* DOPRI5 / 'auto' / 'bdf' without a trajectory, S <= 8 (odelib_amd/csrc/lane.cuh, the
+                     MH kernels): every walker takes its own DOPRI5 step sizes, i.e. the lockstep
+                     algorithm on a group of one.  (The BDF pass is a group of one per walker
+                     in every mode, bdf_lane.cuh.) */
 } Prob;
 
 static void rhs(const Prob* pb, const double* y, double t, const double* ps, double* dy) {
@@ -1287,14 +1288,11 @@ static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double*
       any |= L[l].part;
       if (L[l].part) L[l].a.status |= ST_STIFF;
     }
-    if (any) {
-      if (pb->lane_steps) {
-        for (int l = 0; l < nl; ++l)
-          if (L[l].part) bdf_group(pb, L + l, 1, p + l * MAXP, traj, W);
-      } else {
-        bdf_group(pb, L, nl, p, traj, W);
-      }
-    }
+    /* every handed lane on its own: the device's BDF pass (bdf_lane.cuh) gives each lane
+       its own step size and order, in every kernel */
+    if (any)
+      for (int l = 0; l < nl; ++l)
+        if (L[l].part) bdf_group(pb, L + l, 1, p + l * MAXP, traj, W);
     return;
   }
   for (int l = 0; l < nl; ++l) memcpy(L[l].y0c, L[l].y, sizeof(double) * S);
@@ -1380,12 +1378,8 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
       q->i_ev = 1;
       q->k_ev = q->kobs;
     }
-    if (pb->lane_steps) {
-      for (int l = 0; l < LANES; ++l)
-        if (L[l].part) bdf_group(pb, L + l, 1, p + l * MAXP, traj, W);
-    } else {
-      bdf_group(pb, L, LANES, p, traj, W);
-    }
+    for (int l = 0; l < LANES; ++l) /* a group of one per walker, as the device (bdf_lane.cuh) */
+      if (L[l].part) bdf_group(pb, L + l, 1, p + l * MAXP, traj, W);
   } else {
     for (int l = 0; l < LANES; ++l) L[l].part = L[l].active;
     if (pb->wave_redo) {

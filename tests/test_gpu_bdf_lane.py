@@ -1,4 +1,4 @@
-"""The MH kernels' BDF pass with a step size and an order per lane (csrc/bdf_lane.cuh): the
+"""The MH kernels' BDF pass with a step size and an order per lane (csrc/bdf.cuh): the
 hand-over of 'auto' and method 'bdf' in k_mh / k_mh_tree.
 
 The reference integrates every proposal with its own odeint call (Framework.py:656, one

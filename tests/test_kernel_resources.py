@@ -5,7 +5,7 @@ the chain20 DOPRI5 MH kernel once doubled in time (13.4 vs 6.3 ms per iteration,
 DESIGN.md §3.4 r01k) after unrelated integrator changes pushed it to 432 B/lane of
 scratch.  These budgets catch that at build time: hipcc's kernel-resource-usage remarks
 for the translation units the bench and the C3 configs use, and for the stiff methods' MH
-kernels (k_mh / k_mh_tree with 'auto' and 'bdf', the per-lane BDF pass of csrc/bdf_lane.cuh)
+kernels (k_mh / k_mh_tree with 'auto' and 'bdf', the per-lane BDF pass of csrc/bdf.cuh)
 of every built-in model with at most 8 states.
 """
 import os
@@ -74,8 +74,12 @@ TREE_TWO_I_DOPRI5 = ("k_mh_treeINS_4TwoIELi1E",)
 
 
 def test_two_i_kernels_never_spill(resources):
+    """No two_i kernel touches scratch; the kernels without a stiff method do not spill at
+    all (the 'auto' / 'bdf' kernels run at one wave per SIMD, where a spill lands in AGPRs)."""
     for name, r in resources["inst_two_i.hip"].items():
-        assert r["scratch"] == 0 and r["vgpr_spill"] == 0, (name, r)
+        assert r["scratch"] == 0, (name, r)
+        if not re.search(r"ELi[24]E", name):
+            assert r["vgpr_spill"] == 0, (name, r)
 
 
 @pytest.mark.parametrize("needles,min_occ", [(C1, 4), (C2, 2), (MH_TWO_I_RK4, 4), (MH_TWO_I_DOPRI5, 2),
