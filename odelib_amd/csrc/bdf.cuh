@@ -422,6 +422,11 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
     for (int j = 0; j < kWin; ++j) c += (st.wv[j] <= tn) ? 1 : 0;
     if (c == 0) break;
     crossed = true;
+    // the next window, loaded BEFORE this chunk's row stores: on gfx950 a vector load's
+    // wait also waits for every store issued ahead of it (NT row stores: ~µs)
+    double nw[kWin];
+#pragma unroll
+    for (int j = 0; j < kWin; ++j) nw[j] = pb.times[i + c + j];  // (times[T..] are +inf sentinels)
     for (int j = 0; j < c; ++j) {
       const int g = i + j;
       const bool observed = g == st.nxt;
@@ -448,7 +453,7 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
     }
     i += c;
 #pragma unroll
-    for (int j = 0; j < kWin; ++j) st.wv[j] = pb.times[i + j];  // (times[T..] are +inf sentinels)
+    for (int j = 0; j < kWin; ++j) st.wv[j] = nw[j];
   } while (c == kWin);
   if (crossed) {
     st.nst = 0;

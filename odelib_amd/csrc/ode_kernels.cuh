@@ -941,6 +941,7 @@ constexpr int kGridWin = 8;  // the time grid buffer carries kGridWin + 1 +inf s
 }
 #include "stiff.cuh"
 #include "bdf.cuh"
+#include "bdf_wave.cuh"
 #include "lane.cuh"
 namespace oe {
 
@@ -971,7 +972,10 @@ __device__ __forceinline__ void integrate_walker(const DevProblem& pb, double (&
     static_assert(M::S <= kStiffRegS, "bdf: register path only");
     int k = 0;
     emit<M::S, TRAJ, NT>(pb, 0, y, traj, W, off, active, k, a);
-    integrate_bdf_lane<M, PMAX, TRAJ, NT>(pb, y, kconst(pb.times)[0], 1, k, p, traj, W, w, active, active, a);
+    if constexpr (LANE)  // MH kernels: every chain with its own step sizes and orders (bdf.cuh)
+      integrate_bdf_lane<M, PMAX, TRAJ, NT>(pb, y, kconst(pb.times)[0], 1, k, p, traj, W, w, active, active, a);
+    else  // integrate kernels: the wave-lockstep pass (bdf_wave.cuh), as their DOPRI5
+      integrate_bdf<M, PMAX, TRAJ, NT>(pb, y, kconst(pb.times)[0], 1, k, p, traj, W, w, active, active, a);
   } else if constexpr (METHOD == kAuto && M::S <= kStiffRegS && LANE) {
     // per-lane DOPRI5 whose flagged lanes continue with BDF from their own eviction points
     // (the BDF pass is lane.cuh's tail: it starts from the DOPRI5 pass's live state)

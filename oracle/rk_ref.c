@@ -71,8 +71,10 @@ typedef struct {
                     each lane's states, combined in a tree of lanes (lower lane kept on ties) */
   int lane_steps; /* DOPRI5 / 'auto' / 'bdf' without a trajectory, S <= 8 (odelib_amd/csrc/lane.cuh, the
                      MH kernels): every walker takes its own DOPRI5 step sizes, i.e. the lockstep
-                     algorithm on a group of one.  (The BDF pass is a group of one per walker
-                     in every mode, bdf_lane.cuh.) */
+                     algorithm on a group of one, and method 'bdf' BDF steps and orders per
+                     walker.  (The BDF pass of 'auto' is a group of one per walker in every
+                     mode, odelib_amd/csrc/bdf.cuh; the integrate kernels' method 'bdf' is the
+                     64-lane lockstep group, bdf_wave.cuh.) */
 } Prob;
 
 static void rhs(const Prob* pb, const double* y, double t, const double* ps, double* dy) {
@@ -1378,8 +1380,12 @@ static void integrate_group(const Prob* pb, int64_t W, int64_t g, const double* 
       q->i_ev = 1;
       q->k_ev = q->kobs;
     }
-    for (int l = 0; l < LANES; ++l) /* a group of one per walker, as the device (bdf_lane.cuh) */
-      if (L[l].part) bdf_group(pb, L + l, 1, p + l * MAXP, traj, W);
+    if (pb->lane_steps) { /* the MH kernels: a group of one per walker (bdf.cuh) */
+      for (int l = 0; l < LANES; ++l)
+        if (L[l].part) bdf_group(pb, L + l, 1, p + l * MAXP, traj, W);
+    } else { /* the integrate kernels: the 64-lane wave in lockstep (bdf_wave.cuh) */
+      bdf_group(pb, L, LANES, p, traj, W);
+    }
   } else {
     for (int l = 0; l < LANES; ++l) L[l].part = L[l].active;
     if (pb->wave_redo) {

@@ -148,13 +148,18 @@ GLOO2_CHILD = textwrap.dedent(r"""
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        # RK4: a walker's arithmetic is its own (DOPRI5 shares a step size per 64-walker
-        # group, so there only shard boundaries on group boundaries reproduce one launch)
-        m = product_model("two_i", method="rk4")
+        # every MH chain is integrated on its own (RK4; DOPRI5 and BDF with their own step
+        # sizes per chain), so the shards reproduce one launch whatever their boundaries
+        method = os.environ["OE_METHOD"]
+        m = product_model("two_i", method=method)
         eng = m.engine()
         W = 301  # ragged: 151 + 150 walkers
         theta = np.repeat(np.array([float(m.parameters[p].val) for p in m.get_pnames()])[:, None], W, axis=1)
         theta = theta * np.exp(0.02 * np.random.RandomState(3).standard_normal(theta.shape))
+        if method == "auto":  # stiff chains in both shards: handed to BDF at their own times
+            for w, tau in ((7, 1e5), (150, 1e4), (151, 3e4), (300, 1e5)):
+                theta[4, w] = tau
+            theta[1, [20, 200]] = 1.5e-5
         y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
         walk = np.ones(5, np.uint8)
         pooled, mine = sharded_mh(eng, theta, y0, nits=10, burnin=3, walk_mask=walk, seed=8)
@@ -163,6 +168,8 @@ GLOO2_CHILD = textwrap.dedent(r"""
         if rank == 0:
             ref = eng.mh_run(theta, y0, nits=10, burnin=3, walk_mask=walk, rng="philox", seed=8)
             assert torch.equal(pooled.cpu(), ref["samples"].cpu()), "pooled shards differ from one launch"
+            if method == "auto":
+                assert (ref["status"].cpu().numpy() & 8).any(), "no chain was handed to BDF"
             import pandas as pd
             from odelib_amd.Framework import rawstats
             s = ref["samples"].cpu().numpy()
@@ -177,17 +184,19 @@ GLOO2_CHILD = textwrap.dedent(r"""
 
 
 @pytest.mark.gpu
-def test_two_gloo_ranks_device_engine_pool_equals_one_launch():
+@pytest.mark.parametrize("method", ["rk4", "auto"])
+def test_two_gloo_ranks_device_engine_pool_equals_one_launch(method):
     """World size 2 with the DEVICE engine (verdict r2: the CPU world-2 test drives the C
     restatement): two ranks on one GPU (gloo; RCCL refuses two ranks per device), each
     running its shard through oe_mh_run (in speculative rounds: sharded_mh's default, 151
     chains leave the device idle), pooled by the all-gather and the rawstats all-reduces —
-    equal to one sequential 301-walker launch bit for bit."""
+    equal to one sequential 301-walker launch bit for bit.  'auto' (the drop-in default)
+    with stiff chains in both shards: the chains handed to BDF are bitwise too."""
     port = str(_free_port())
     procs = []
     for r in range(2):
         env = dict(os.environ, ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RANK=str(r), WORLD_SIZE="2",
-                   LOCAL_RANK=str(r))
+                   LOCAL_RANK=str(r), OE_METHOD=method)
         procs.append(subprocess.Popen([sys.executable, "-c", GLOO2_CHILD], cwd=ROOT, env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=150) for p in procs]
@@ -196,22 +205,27 @@ def test_two_gloo_ranks_device_engine_pool_equals_one_launch():
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_rehearsal():
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_multi_rank_rehearsal(n):
     """bench.py's multi-rank path as the driver launches it (torchrun child launch from
-    --gpus 2), rehearsed on one GPU over gloo: the line reports 2 GPUs, the headline counts
-    both ranks' walkers, and the C4 leg shards 1 048 576 walkers and pools the posterior."""
+    --gpus N), rehearsed on one GPU over gloo for N = 2 and for the driver's N = 8
+    (Framework.py:779-780's chain pool, :1037's concat): the line reports N GPUs, the
+    headline counts every rank's walkers, and the C4 leg shards 1 048 576 walkers into N
+    contiguous shards (131 072 per rank at N = 8) and pools the 4.11 GB posterior."""
     import json
     env = dict(os.environ, ODELIB_BENCH_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "3", "--warmup", "1",
                         "--warmup-ms", "5", "--no-extra-configs", "--no-pmc", "--mcmc-iters", "5", "--c4-steps", "2"],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=840)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["config"]["walkers_total"] == 2 * 65536
+    assert line["n_gpus"] == n and line["config"]["walkers_total"] == n * 65536
     c4 = line["other_configs"]["C4"]
-    assert c4["walkers_total"] == 1 << 20 and c4["walkers_per_gpu"] == 1 << 19 and c4["n_gpus"] == 2
+    assert c4["walkers_total"] == 1 << 20 and c4["walkers_per_gpu"] == (1 << 20) // n and c4["n_gpus"] == n
     assert c4["allgather"]["bytes_gathered"] == 49 * 10 * (1 << 20) * 8
+    assert c4["allgather"]["world_size"] == n
     assert c4["integrate"]["chi_finite"]
 
 
