@@ -254,7 +254,7 @@ __device__ __forceinline__ bool bdf_attempt(const DevProblem& pb, BdfState<M::S>
           if (kk > 0) {
             rate = dn / dold;
             const double pw = (kk == 1) ? (rate * rate) * rate : (kk == 2) ? rate * rate : rate;
-            if (!(rate < 1.0) || pw / (1.0 - rate) * dn > ntol) { fail = true; ok = false; }
+            if (!(rate < 1.0) || pw * dn > ntol * (1.0 - rate)) { fail = true; ok = false; }
           }
           if (ok) {
 #pragma unroll
@@ -262,7 +262,7 @@ __device__ __forceinline__ bool bdf_attempt(const DevProblem& pb, BdfState<M::S>
               yn[s] = yn[s] + dy[s];
               d[s] = d[s] + dy[s];
             }
-            if (dn == 0.0 || (kk > 0 && rate / (1.0 - rate) * dn < ntol)) conv = true;
+            if (dn == 0.0 || (kk > 0 && rate * dn < ntol * (1.0 - rate))) conv = true;
             dold = dn;
           }
         }

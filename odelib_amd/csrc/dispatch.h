@@ -126,9 +126,9 @@ template <class M>
 struct SplitOf { static constexpr int K = 0; };
 template <int N>
 struct SplitOf<Chain<N>> { static constexpr int K = split_lanes_chain<N>(); };
-#ifdef OE_SPLIT_TWOI  // measurement builds: two_i (Chain<4>'s RHS, operation for operation) over 2 lanes
+#ifdef OE_SPLIT_TWOI  // measurement builds: two_i (Chain<4>'s RHS, operation for operation) over 2 or 4 lanes
 template <>
-struct SplitOf<TwoI> { static constexpr int K = 2; };
+struct SplitOf<TwoI> { static constexpr int K = OE_SPLIT_TWOI; };
 #endif
 
 template <class M, int METHOD>

@@ -64,14 +64,18 @@ __device__ __forceinline__ void chain_rhs_split(const double (&y)[N / K], const 
   const double prev = dpp_f64<QuadCtl<K>::prev>(y[m - 1]);
   const double inf = phi * Sv * V;
   const double bl = beta * lam;
+  // roles by the element's GLOBAL index g = r·m + j (with m = 1 or 2 the I1 / I(N-2) roles sit
+  // on inner lanes); r from the lane flags for K = 2, from the lane id otherwise
+  const int r = (K == 2) ? (first_lane ? 0 : 1) : (int)(__lane_id() & (K - 1));
 #pragma unroll
   for (int j = 0; j < m; ++j) {
+    const int g = r * m + j;
     const double ym1 = (j == 0) ? prev : y[j - 1];
     double A = tau, B = ym1, C = tau * y[j];  // tau*I(k-1) - tau*Ik
-    if (j == 0 && first_lane) { A = mu; B = Sv; C = inf; }                        // mu*S - phi*S*V
-    if (j == 1 && first_lane) { A = -tau; B = y[j]; C = -inf; }                   // phi*S*V - tau*I1
-    if (j == m - 2 && last_lane) C = lam * y[j];                                  // tau*I(N-3) - lam*I(N-2)
-    if (j == m - 1 && last_lane) { A = bl; C = inf; }                             // beta*lam*I(N-2) - phi*S*V
+    if (g == 0) { A = mu; B = Sv; C = inf; }                                      // mu*S - phi*S*V
+    if (g == 1) { A = -tau; B = y[j]; C = -inf; }                                 // phi*S*V - tau*I1
+    if (g == N - 2) C = lam * y[j];                                               // tau*I(N-3) - lam*I(N-2)
+    if (g == N - 1) { A = bl; C = inf; }                                          // beta*lam*I(N-2) - phi*S*V
     dy[j] = fma(A, B, -C);
   }
 }

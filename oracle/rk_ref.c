@@ -1117,13 +1117,13 @@ static void bdf_group(const Prob* pb, Lane* L, int nl, const double* p, double* 
           if (k > 0) {
             rate = dn / b->dold;
             const double pw = (k == 1) ? (rate * rate) * rate : (k == 2) ? rate * rate : rate;
-            if (!(rate < 1.0) || pw / (1.0 - rate) * dn > ntol) { b->fail = 1; continue; }
+            if (!(rate < 1.0) || pw * dn > ntol * (1.0 - rate)) { b->fail = 1; continue; }
           }
           for (int s = 0; s < S; ++s) {
             b->yn[s] = b->yn[s] + dy[s];
             b->d[s] = b->d[s] + dy[s];
           }
-          if (dn == 0.0 || (k > 0 && rate / (1.0 - rate) * dn < ntol)) b->conv = 1;
+          if (dn == 0.0 || (k > 0 && rate * dn < ntol * (1.0 - rate))) b->conv = 1;
           b->dold = dn;
         }
       }

@@ -1,5 +1,7 @@
-"""One wave, one stiff lane: method 'bdf' chi-only integrates of a single walker, for
-rocprofv3 PMC passes (SQ counters per BDF step of a lone lane) and wall timing.
+"""One wave, one stiff lane: method 'bdf' on a single walker — the per-lane pass (bdf.cuh, the
+a-priori fit of an mh_run with nits = 1, kernel k_mh) or the wave-lockstep pass (bdf_wave.cuh,
+a chi-only integrate, k_integrate) — for rocprofv3 PMC passes (SQ counters per BDF step of a
+lone lane) and wall timing.
 
     python tools/bdf_one.py --case tau1e5 --reps 5
     rocprofv3 --pmc SQ_INSTS_VALU ... --kernel-include-regex k_integrate -- python tools/bdf_one.py
@@ -25,6 +27,7 @@ def main():
     ap.add_argument("--case", default="tau1e5", choices=list(CASES))
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--method", default="bdf")
+    ap.add_argument("--kernel", default="lane", choices=["lane", "wave"])
     args = ap.parse_args()
     import numpy as np
     from helpers import product_model
@@ -39,9 +42,12 @@ def main():
     steps = b["accepted"] + b["rejected_error"] + b["rejected_newton"]
     ms = []
     for _ in range(args.reps):
-        eng.integrate(y0, th, trajectory=False)
+        if args.kernel == "lane":
+            eng.mh_run(th, y0, nits=1, burnin=0, walk_mask=np.ones(5, np.uint8))
+        else:
+            eng.integrate(y0, th, trajectory=False)
         ms.append(eng.last_kernel_ms())
-    print(json.dumps({"case": args.case, "method": args.method, "lib": os.environ.get("ODELIB_AMD_LIB", "default"),
+    print(json.dumps({"case": args.case, "method": args.method, "kernel": args.kernel, "lib": os.environ.get("ODELIB_AMD_LIB", "default"),
                       "bdf_steps": steps, "detail": b, "kernel_ms_min": min(ms),
                       "us_per_step": 1e3 * min(ms) / max(steps, 1)}), flush=True)
 
