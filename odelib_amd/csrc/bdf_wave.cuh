@@ -394,6 +394,43 @@ __device__ __forceinline__ void bdf_select(BdfState<S>& st, int q, const BdfAcce
   st.lu_ok = false;
 }
 
+// The same selection with the order a template parameter (constant divisions in the roots,
+// unrolled loops, change_D at a constant order; the same operations): 11 % faster on 65 536
+// walkers with trajectories (2.63 vs 2.95 ms).  In r04 a build of it failed the chain8 'bdf'
+// parity test deterministically while every other stiff case stayed bitwise (profiles/NOTES.md
+// r04n); rebuilt in r05 it is bitwise on every stiff test (NOTES.md round 5), so it is the
+// default again; OE_BDF_WAVE_SELECT_TEMPLATED=0 builds the order-generic selection.
+#ifndef OE_BDF_WAVE_SELECT_TEMPLATED
+#define OE_BDF_WAVE_SELECT_TEMPLATED 1
+#endif
+template <int S, int Q>
+__device__ __forceinline__ void bdf_select_q(BdfState<S>& st, const BdfAccepted& acc) {
+  using namespace bdf;
+  const bool voter = st.live;
+  if (__ballot(voter) == 0ull) return;
+  const double em = wave_max(voter ? acc.em_l : 0.0), ep = wave_max(voter ? acc.ep_l : 0.0);
+  double fm = 0.0, fp = 0.0;
+  if constexpr (Q > 1) fm = bdfl::inv_root<Q>(em);
+  const double fe = bdfl::inv_root<Q + 1>(acc.en);
+  if constexpr (Q < kMaxQ) fp = bdfl::inv_root<Q + 2>(ep);
+  int dq = 0;
+  double fmx = fm;
+  if (fe > fmx) { fmx = fe; dq = 1; }
+  if (fp > fmx) { fmx = fp; dq = 2; }
+  const double factor = fmin(10.0, acc.safety * fmx);
+  st.h = acc.h * factor;
+  if (dq == 0) {
+    if constexpr (Q > 1) change_D<S>(st.D, Q - 1, factor);
+  } else if (dq == 1) {
+    change_D<S>(st.D, Q, factor);
+  } else {
+    if constexpr (Q < kMaxQ) change_D<S>(st.D, Q + 1, factor);
+  }
+  st.order = Q + dq - 1;
+  st.neq = 0;
+  st.lu_ok = false;
+}
+
 // BDF integration of the lanes with `part` set from their own (t, y, grid index i,
 // observation index k) with their accumulators as they are; the others sit out (no vote,
 // no output).  y is the final state (the last grid point's) on return.
@@ -472,7 +509,19 @@ __device__ __forceinline__ void integrate_bdf(const DevProblem& pb, double (&y)[
     }
     if (ok) {
       bdf_output<S, TRAJ, NT>(pb, st, q, acc.h, y, traj, W, w, active, a);
+#if OE_BDF_WAVE_SELECT_TEMPLATED
+      if (acc.select) {
+        switch (q) {
+          case 1: bdf_select_q<S, 1>(st, acc); break;
+          case 2: bdf_select_q<S, 2>(st, acc); break;
+          case 3: bdf_select_q<S, 3>(st, acc); break;
+          case 4: bdf_select_q<S, 4>(st, acc); break;
+          default: bdf_select_q<S, 5>(st, acc); break;
+        }
+      }
+#else
       if (acc.select) bdf_select<S>(st, q, acc);
+#endif
     }
     // budget: a lane that needs more than `budget` steps inside one output interval, or a
     // step below hmin, is abandoned (MAXSTEP, NaN for the rest of its grid)
