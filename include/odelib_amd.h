@@ -72,8 +72,10 @@ enum {
                               times.  n_states <= 32 */
   OE_METHOD_BDF = 4      /* LSODA's stiff branch for every walker: variable-order (1..5) BDF in
                             scipy's fixed-leading-coefficient form, max norm, modified Newton on an
-                            exact (dual-number) Jacobian; walkers share the step size and order per
-                            wave.  n_states <= 8 */
+                            exact (dual-number) Jacobian.  n_states <= 8.  Trajectory / chi kernels
+                            (oe_integrate): walkers share the step size and order per wave.  MH
+                            kernels (oe_mh_run): a step size and an order per walker, so a chain
+                            does not depend on the chains that share its wavefront */
 };
 
 /* built-in right-hand sides (demo notebook models + synthetic chain) */
@@ -225,9 +227,11 @@ typedef struct {
                                  round integrates every proposal the next d accept/reject
                                  decisions can lead to (2^d - 1 per chain) at once, then keeps
                                  each chain's actual path: the same Markov chain, the same draws
-                                 in the same order.  RK4: bitwise the chains of speculate = 0;
-                                 DOPRI5 / auto: within the integration tolerance (a wave's 64
-                                 lanes share one step size, and they are other proposals here).
+                                 in the same order.  RK4, and DOPRI5 / auto / BDF with
+                                 n_states <= 8 (a step size per lane): bitwise the chains of
+                                 speculate = 0; larger models: within the integration tolerance
+                                 (a wave's 64 lanes share one step size, and they are other
+                                 proposals here).
                                  Every MH kernel: built-in and hipRTC models, one lane or split
                                  over K lanes per chain (the depth then counts K lanes per
                                  proposal). */

@@ -34,13 +34,13 @@ namespace oe {
 
 // AUTO (S <= kStiffRegS): the stiffness test of integrate_dopri5 hands the lane over at
 // its eviction point, as does the step budget; the BDF pass at the end continues it from
-// the loop's live state (t, y, grid index, observation index, accumulators).  (With that
-// state copied into a Resume struct and the BDF pass run by the caller, as the lockstep
-// path does, the MH kernels — 400+ SGPRs spilled to VGPR lanes — returned garbage from the
-// BDF pass for the handed lanes, and any printf or extra store around the call made it
-// right again: a code-generation fragility, not an algorithm difference.  This shape is
-// bitwise the C restatement in every kernel: tests/test_gpu_stiff.py,
-// test_gpu_speculative.py.)
+// the loop's live state (t, y, grid index, observation index, accumulators) with a step
+// size and an order of its own (integrate_bdf_lane, bdf.cuh), so a handed lane's result
+// does not depend on its wave-mates.  The call sits inside the DOPRI5 loop's exit path
+// rather than in the caller: round 4's copy of the state into a Resume struct for a BDF
+// pass run by the caller miscompiled in the MH kernels (400+ SGPRs spilled to VGPR lanes).
+// This shape is bitwise the C restatement (oracle/rk_ref.c, lane mode) in every kernel:
+// tests/test_gpu_bdf_lane.py, test_gpu_stiff.py, test_gpu_speculative.py.
 template <class M, int PMAX, bool AUTO>
 __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, double (&y)[M::S],
                                                       const double (&p)[PMAX], int64_t W, uint32_t off,

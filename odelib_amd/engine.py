@@ -357,9 +357,9 @@ class Engine:
         ``speculate``: speculative rounds for small ensembles (oe_mh_args.speculate): 0 off,
         "auto" (or -1) the library's depth (off when the chains fill the device), d >= 2
         iterations per round — every proposal the next d decisions can lead to is integrated
-        at once and each chain keeps its own path: RK4 and DOPRI5 chains are bitwise those
-        of ``speculate=0`` (every MH lane takes its own DOPRI5 steps), and so are ``auto``
-        chains whose proposals never reach the BDF hand-over.  ``last_mh_depth()``
+        at once and each chain keeps its own path: RK4, and DOPRI5 / ``auto`` / ``bdf`` chains
+        of models with <= 8 states, are bitwise those of ``speculate=0`` (every MH lane takes
+        its own steps, BDF ones included).  ``last_mh_depth()``
         reports the depth used."""
         torch = self.torch
         pb = self.problem
