@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--methods", nargs="+", default=["dopri5", "auto", "rosenbrock"])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--trajectory", type=int, default=1)
+    ap.add_argument("--contiguous", action="store_true", help="the stiff walkers are walkers 0..n-1 (one wave's lanes)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -44,6 +45,8 @@ def main():
             th = base.copy()
             n_stiff = int(round(frac * W))
             lanes = np.random.RandomState(7).choice(W, n_stiff, replace=False) if n_stiff else []
+            if args.contiguous:
+                lanes = np.arange(n_stiff)
             if n_stiff:
                 th[4, lanes] = tau
             theta = torch.as_tensor(th, device=dev).contiguous()
