@@ -161,15 +161,27 @@ template <int Q>
 __device__ __forceinline__ double ir_c(int r) {
   static_assert(Q >= 1 && Q <= 6, "order");
   if constexpr (Q == 1) return 1.0;
-  if constexpr (Q == 2) return r == 0 ? 1.0 : 0.7071067811865476;
-  if constexpr (Q == 3) return r == 0 ? 1.0 : r == 1 ? 0.7937005259840998 : 0.6299605249474366;
-  if constexpr (Q == 4) return r == 0 ? 1.0 : r == 1 ? 0.8408964152537145 : r == 2 ? 0.7071067811865476 : 0.5946035575013605;
-  if constexpr (Q == 5)
-    return r == 0 ? 1.0 : r == 1 ? 0.8705505632961241 : r == 2 ? 0.757858283255199 : r == 3 ? 0.6597539553864471
-                                                                                    : 0.5743491774985174;
-  if constexpr (Q == 6)
-    return r == 0 ? 1.0 : r == 1 ? 0.8908987181403393 : r == 2 ? 0.7937005259840998 : r == 3 ? 0.7071067811865476
-           : r == 4 ? 0.6299605249474366 : 0.5612310241546865;
+  if constexpr (Q == 2) {
+    constexpr double c[2] = {1.0, 0.7071067811865476};
+    return dp::select_r(r, c);
+  }
+  if constexpr (Q == 3) {
+    constexpr double c[3] = {1.0, 0.7937005259840998, 0.6299605249474366};
+    return dp::select_r(r, c);
+  }
+  if constexpr (Q == 4) {
+    constexpr double c[4] = {1.0, 0.8408964152537145, 0.7071067811865476, 0.5946035575013605};
+    return dp::select_r(r, c);
+  }
+  if constexpr (Q == 5) {
+    constexpr double c[5] = {1.0, 0.8705505632961241, 0.757858283255199, 0.6597539553864471, 0.5743491774985174};
+    return dp::select_r(r, c);
+  }
+  if constexpr (Q == 6) {
+    constexpr double c[6] = {1.0, 0.8908987181403393, 0.7937005259840998, 0.7071067811865476, 0.6299605249474366,
+                             0.5612310241546865};
+    return dp::select_r(r, c);
+  }
 }
 // bdf::inv_root for a compile-time q: the same operations (constant division, unrolled
 // powers), the same bits

@@ -456,6 +456,21 @@ __device__ __forceinline__ Tab load_tab() {
   return t;
 }
 
+// c[r] for a per-lane r in [0, N), N <= 8, as selects on r's bits.  (A chain of
+// r == k ? … ternaries becomes a switch, lowered for a divergent r to compare-and-branch
+// blocks with EXEC-mask bookkeeping: ~20 scalar instructions and four branches, which a
+// lone wave issues one per slot.)
+template <int N>
+__device__ __forceinline__ double select_r(int r, const double (&c)[N]) {
+  static_assert(N >= 1 && N <= 8, "select_r: at most 8 entries");
+  auto at = [&](int k) { return c[k < N ? k : N - 1]; };
+  const bool b0 = (r & 1) != 0, b1 = (r & 2) != 0, b2 = (r & 4) != 0;
+  const double l0 = b0 ? at(1) : at(0), l1 = b0 ? at(3) : at(2);
+  const double l2 = b0 ? at(5) : at(4), l3 = b0 ? at(7) : at(6);
+  const double m0 = b1 ? l1 : l0, m1 = b1 ? l3 : l2;
+  return b2 ? m1 : m0;
+}
+
 // x^(-1/5) for finite x > 0 (the step controller's err^(-1/5) and HINIT's
 // (0.01/dm)^(1/5)).  Only exact scalings (frexp/ldexp) and IEEE mul/fma, so the host
 // restatement (oracle/rk_ref.c inv_fifth_root) reproduces it bit for bit — libm's and
@@ -474,9 +489,8 @@ __device__ __forceinline__ double inv_fifth_root(double x) {
     const double y5 = (y2 * y2) * y;
     y = (y * fma(-m, y5, 6.0)) * 0.2;
   }
-  const double c = r == 0 ? 1.0 : r == 1 ? 0.8705505632961241 : r == 2 ? 0.757858283255199
-                 : r == 3 ? 0.6597539553864471 : 0.5743491774985174;
-  return ldexp(c * y, -q);
+  constexpr double kC[5] = {1.0, 0.8705505632961241, 0.757858283255199, 0.6597539553864471, 0.5743491774985174};
+  return ldexp(select_r(r, kC) * y, -q);
 }
 
 // inv_fifth_root of a WAVE-UNIFORM x (the step controller's err): the exponent part

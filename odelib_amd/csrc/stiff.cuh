@@ -226,8 +226,8 @@ __device__ __forceinline__ double inv_fourth_root(double x) {
     const double y2 = y * y;
     y = (y * fma(-m, y2 * y2, 5.0)) * 0.25;
   }
-  const double c = r == 0 ? 1.0 : r == 1 ? 0.8408964152537145 : r == 2 ? 0.7071067811865476 : 0.5946035575013605;
-  return ldexp(c * y, -q);
+  constexpr double kC[4] = {1.0, 0.8408964152537145, 0.7071067811865476, 0.5946035575013605};
+  return ldexp(dp::select_r(r, kC) * y, -q);
 }
 
 // LU with threshold partial pivoting: column k is pivoted only when |a_kk| < 0.1 x the
