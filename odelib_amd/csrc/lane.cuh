@@ -183,6 +183,9 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
           }
         }
       }
+      // the controller's safe·err^(-1/5), shared by the accept and reject paths (a wave whose
+      // lanes split between them would otherwise run the root twice)
+      const double sfe = safe * inv_fifth_root(err > 0.0 ? err : 1.0);
       if (!handed && err <= 1.0) {  // an accepted step (not handed over at its start)
         const double tn = last ? tend : t + h;
         if (tn >= t_seg) {  // the step that crosses the segment's time: keep its coefficients
@@ -220,14 +223,14 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
 #pragma unroll
         for (int s = 0; s < S; ++s) { y[s] = yn[s]; k1[s] = k7[s]; }
         t = tn;
-        double fac = (err > 0.0) ? safe * inv_fifth_root(err) : facmax;
+        double fac = (err > 0.0) ? sfe : facmax;
         fac = fmin(facmax, fmax(facmin, fac));
         if (last_rej) fac = fmin(fac, 1.0);
         h = h * fac;
         last_rej = false;
         if (i >= pb.T) done = true;
       } else if (!handed) {
-        h = h * fmax(facmin, safe * inv_fifth_root(err));
+        h = h * fmax(facmin, sfe);
         last_rej = true;
       }
       // ---- budget: the lane leaves (not after the last grid point) ----
