@@ -243,6 +243,41 @@ __device__ __forceinline__ DTab<S> dtab_column() {
 #endif
 }
 
+// Measurement builds (tools/build_alt.sh … -DOE_BDF_CLOCKS=1, tools/bdf_phases.py): shader
+// cycles (s_memtime) per phase of the per-lane step, summed over a lane's pass and printed
+// at its end — for one-walker runs.  0 in every shipped build.
+#ifndef OE_BDF_CLOCKS
+#define OE_BDF_CLOCKS 0
+#endif
+enum BdfPhase { kPhPredict, kPhFactor, kPhNewton, kPhErr, kPhDiff, kPhGrid, kPhSelect, kPhFail, kPhN };
+struct BdfClk {
+#if OE_BDF_CLOCKS
+  uint64_t c[kPhN], last;
+  uint32_t n[kPhN];
+  __device__ __forceinline__ void start() {
+    for (int j = 0; j < kPhN; ++j) { c[j] = 0; n[j] = 0; }
+    last = __builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void mark(int ph) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    c[ph] += now - last;
+    n[ph] += 1;
+    last = now;
+  }
+#else
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void mark(int) {}
+#endif
+};
+
+#if OE_BDF_CLOCKS
+// the s_memtime at which each wave of the workgroup entered its kernel (k_integrate, k_mh)
+__device__ __forceinline__ uint64_t* bdf_clk_wave_start() {
+  __shared__ uint64_t t[16];
+  return t;
+}
+#endif
+
 template <int S>
 struct BdfLane {
   DTab<S> D;                 // backward differences (scipy's D), in LDS
@@ -253,6 +288,7 @@ struct BdfLane {
   int q, neq, nst;           // order, steps at this h and q, steps since the last grid point
   int i, k, nxt;             // next grid index, next observation record, its grid index
   bool live, lu_ok, fresh, refac, swp;
+  BdfClk clk;
 };
 
 // scipy's change_D at a compile-time order Q (bdf::change_D's operations)
@@ -412,8 +448,10 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
     st.h = st.h * factor;
     bdfl_change_D<S, Q>(st.D, factor);
     st.neq = 0;
+    st.clk.mark(kPhFail);
     return;
   }
+  st.clk.mark(kPhErr);
   ++st.neq;
   st.fresh = false;
   const double tn = st.t + st.h;
@@ -427,6 +465,7 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
 #pragma unroll
     for (int s = 0; s < S; ++s) st.D(j, s) = st.D(j, s) + st.D(j + 1, s);
   ++st.nst;
+  st.clk.mark(kPhDiff);
   // grid points in (t, tn]: counted on the window, a window's worth at a time; the rows
   // (TRAJ), the observed points and T − 1 (the final state) from the interpolant
   int i = st.i, c;
@@ -437,17 +476,22 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
     for (int j = 0; j < kWin; ++j) c += (st.wv[j] <= tn) ? 1 : 0;
     if (c == 0) break;
     crossed = true;
-    // the next window, loaded BEFORE this chunk's row stores: on gfx950 a vector load's
-    // wait also waits for every store issued ahead of it (NT row stores: ~µs)
-    double nw[kWin];
+    // the next window goes straight into st.wv, loaded BEFORE this chunk's row stores (on
+    // gfx950 a vector load's wait also waits for every store issued ahead of it) and first
+    // read by the next step's count: neither the load's latency nor the stores' is waited for
+    // here (a window copied in at the end of the chunk waited ~1 000 cycles per step, 18 % of
+    // a lone lane's step: tools/bdf_phases.py).  The chunk reads the old window from ow.
+    double ow[kWin];
 #pragma unroll
-    for (int j = 0; j < kWin; ++j) nw[j] = pb.times[i + c + j];  // (times[T..] are +inf sentinels)
+    for (int j = 0; j < kWin; ++j) ow[j] = st.wv[j];
+#pragma unroll
+    for (int j = 0; j < kWin; ++j) st.wv[j] = pb.times[i + c + j];  // (times[T..] are +inf sentinels)
     for (int j = 0; j < c; ++j) {
       const int g = i + j;
       const bool observed = g == st.nxt;
       if (TRAJ || observed || g == pb.T - 1) {
         double yo[S];
-        bdfl_interp<S, Q>(st, tn, pick(st.wv, j), yo);
+        bdfl_interp<S, Q>(st, tn, pick(ow, j), yo);
         if (TRAJ || observed) track_min<S>(yo, a);
         if constexpr (TRAJ) {
           if (tc.active) {
@@ -467,8 +511,6 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
       }
     }
     i += c;
-#pragma unroll
-    for (int j = 0; j < kWin; ++j) st.wv[j] = nw[j];
   } while (c == kWin);
   if (crossed) {
     st.nst = 0;
@@ -476,10 +518,12 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
     if (i >= pb.T) {  // past the last grid point: done (y holds its interpolant)
       st.t = tn;
       st.live = false;
+      st.clk.mark(kPhGrid);
       return;
     }
   }
   st.t = tn;
+  st.clk.mark(kPhGrid);
   if (st.neq >= Q + 1) {  // order and step selection (scipy's rule, capped at 10)
     double fm = 0.0, fp = 0.0;
     if constexpr (Q > 1) {
@@ -511,6 +555,7 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
     st.q = Q + dq - 1;
     st.neq = 0;
     st.lu_ok = false;
+    st.clk.mark(kPhSelect);
   }
 }
 
@@ -532,6 +577,7 @@ __device__ __forceinline__ void bdfl_step(const DevProblem& pb, BdfLane<M::S>& s
   double rs[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) rs[s] = 1.0 / fma(rtol, fabs(yp[s]), atol);
+  st.clk.mark(kPhPredict);
   if (!st.lu_ok || st.refac) {  // at the current state (new h or q), or at the predictor (retry)
     double fy[S];
 #pragma unroll
@@ -540,6 +586,7 @@ __device__ __forceinline__ void bdfl_step(const DevProblem& pb, BdfLane<M::S>& s
     st.lu_ok = true;
     st.fresh = true;
     st.refac = false;
+    st.clk.mark(kPhFactor);
   }
   // ---- B: modified Newton (every live lane, whatever its order) ----
   const double tn = st.t + st.h;
@@ -594,6 +641,7 @@ __device__ __forceinline__ void bdfl_step(const DevProblem& pb, BdfLane<M::S>& s
       }
     }
   }
+  st.clk.mark(kPhNewton);
   if (!conv) {
     if (!st.fresh) {  // failed on older factors: this attempt again, on factors at the predictor
       st.refac = true;
@@ -603,6 +651,7 @@ __device__ __forceinline__ void bdfl_step(const DevProblem& pb, BdfLane<M::S>& s
     bdfl_change_D<S>(st.D, st.q, 0.5);
     st.neq = 0;
     st.lu_ok = false;
+    st.clk.mark(kPhFail);
     return;
   }
   // ---- C ----
@@ -686,6 +735,10 @@ __device__ __forceinline__ void integrate_bdf_lane(const DevProblem& pb, double 
   st.fresh = false;
   st.refac = false;
   st.swp = false;
+  st.clk.start();
+#if OE_BDF_CLOCKS
+  const uint64_t t_entry = st.clk.last;
+#endif
   while (__ballot(st.live) != 0ull) {
     if (st.live) {
       bdfl_step<M, PMAX, TRAJ, NT>(pb, st, p, y, oc, tc, a);
@@ -728,6 +781,15 @@ __device__ __forceinline__ void integrate_bdf_lane(const DevProblem& pb, double 
     }
   }
   if (part) check_finite(y, a);
+#if OE_BDF_CLOCKS
+  if (part)
+    printf("bdf_clocks lane %d since_wave_start %lu bdf_pass %lu predict %lu %u factor %lu %u newton %lu %u "
+           "err %lu %u diff %lu %u grid %lu %u select %lu %u fail %lu %u\n",
+           (int)w, t_entry - bdf_clk_wave_start()[threadIdx.x >> 6], __builtin_amdgcn_s_memtime() - t_entry,
+           st.clk.c[0], st.clk.n[0], st.clk.c[1], st.clk.n[1], st.clk.c[2], st.clk.n[2], st.clk.c[3],
+           st.clk.n[3], st.clk.c[4], st.clk.n[4], st.clk.c[5], st.clk.n[5], st.clk.c[6], st.clk.n[6], st.clk.c[7],
+           st.clk.n[7]);
+#endif
 }
 
 }  // namespace oe

@@ -1094,6 +1094,9 @@ __global__ void __launch_bounds__(256)
     k_integrate(const DevProblem pb, const IntegrateArgs ia) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
+#if OE_BDF_CLOCKS
+  if ((threadIdx.x & 63) == 0) bdf_clk_wave_start()[threadIdx.x >> 6] = __builtin_amdgcn_s_memtime();
+#endif
   const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x, ia.xcd_remap) : (int64_t)blockIdx.x;
   int64_t gw = blk * blockDim.x + threadIdx.x;
   bool idle = false;
@@ -1497,6 +1500,9 @@ __global__ void __launch_bounds__(256)
     k_mh(const DevProblem pb, const MHArgs ma) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
+#if OE_BDF_CLOCKS
+  if ((threadIdx.x & 63) == 0) bdf_clk_wave_start()[threadIdx.x >> 6] = __builtin_amdgcn_s_memtime();
+#endif
   const int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = gw < ma.W;
   const int64_t w = active ? gw : ma.W - 1;
@@ -1660,6 +1666,9 @@ __global__ void __launch_bounds__(256)
     k_mh_tree(const DevProblem pb, const MHTreeArgs ta) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
+#if OE_BDF_CLOCKS
+  if ((threadIdx.x & 63) == 0) bdf_clk_wave_start()[threadIdx.x >> 6] = __builtin_amdgcn_s_memtime();
+#endif
   const MHArgs& ma = ta.m;
   const int64_t W = ma.W;
   const int P = pb.P;
