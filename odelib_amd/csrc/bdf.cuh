@@ -245,7 +245,8 @@ __device__ __forceinline__ DTab<S> dtab_column() {
 
 // Measurement builds (tools/build_alt.sh … -DOE_BDF_CLOCKS=1, tools/bdf_phases.py): shader
 // cycles (s_memtime) per phase of the per-lane step, summed over a lane's pass and printed
-// at its end — for one-walker runs.  0 in every shipped build.
+// at its end — for one-walker runs; =2: no printf, the lane's chi / R² outputs carry the
+// cycles from its wave's start to the pass and in the pass.  0 in every shipped build.
 #ifndef OE_BDF_CLOCKS
 #define OE_BDF_CLOCKS 0
 #endif
@@ -781,7 +782,14 @@ __device__ __forceinline__ void integrate_bdf_lane(const DevProblem& pb, double 
     }
   }
   if (part) check_finite(y, a);
-#if OE_BDF_CLOCKS
+#if OE_BDF_CLOCKS == 2  // no printf (a hostcall per lane perturbs a many-lane launch): the lane's
+                        // chi / R² outputs carry the cycles before the pass and in it
+  if (part) {
+    a.chi = (double)(t_entry - bdf_clk_wave_start()[threadIdx.x >> 6]);
+    a.ssres = (double)(__builtin_amdgcn_s_memtime() - t_entry);
+    a.nvalid = 1;
+  }
+#elif OE_BDF_CLOCKS
   if (part)
     printf("bdf_clocks lane %d since_wave_start %lu bdf_pass %lu predict %lu %u factor %lu %u newton %lu %u "
            "err %lu %u diff %lu %u grid %lu %u select %lu %u fail %lu %u\n",

@@ -22,6 +22,8 @@ from helpers import product_model
 th = np.array([7.475e-9, 1.069e-7, 19.73, 1.934, 1e5])[:, None]
 mode = sys.argv[1]
 m = product_model("two_i", method="bdf" if mode == "mh_bdf" else "auto")
+# modes: mh_bdf | integrate_auto_traj (NT row stores) | integrate_auto_traj_temporal |
+# integrate_auto_nortraj (chi only) | stiffmix2
 eng = m.engine()
 y0 = np.asarray(m.get_inits(), float)[:, None]
 if mode == "stiffmix":  # bench.py's C2-stiffmix: 65 536 synthetic walkers, 0.1 %% with tau = 1e5
@@ -30,20 +32,47 @@ if mode == "stiffmix":  # bench.py's C2-stiffmix: 65 536 synthetic walkers, 0.1 
     th = bench.synthetic_walkers(W, 5)
     th[4, np.random.RandomState(7).choice(W, 66, replace=False)] = 1e5
     y0 = np.repeat(y0, W, axis=1)
+if mode == "stiffmix2":  # -DOE_BDF_CLOCKS=2 library: cycles in the chi / R² outputs
+    import bench
+    W = 65536
+    th = bench.synthetic_walkers(W, 5)
+    lanes = np.random.RandomState(7).choice(W, 66, replace=False)
+    th[4, lanes] = 1e5
+    y0 = np.repeat(y0, W, axis=1)
+    for _ in range(3):
+        out = eng.integrate(y0, th, trajectory=True, sync=True)
+    chi, ss, st = (out[k].cpu().numpy() for k in ("chi", "ssres", "status"))
+    stiff = np.nonzero(st & 8)[0]
+    rows = sorted(((int(chi[w]), int(ss[w]), int(w), int(w) // 64) for w in stiff), key=lambda r: -(r[0] + r[1]))
+    import json
+    print("stiffmix2", eng.last_kernel_ms(), json.dumps(rows), flush=True)
+    sys.exit(0)
 for _ in range(2):
     if mode == "mh_bdf":
         eng.mh_run(th, y0, nits=1, burnin=0, walk_mask=np.ones(5, np.uint8))
     else:
-        eng.integrate(y0, th, trajectory=True, sync=True)
+        eng.integrate(y0, th, trajectory=mode != "integrate_auto_nortraj", sync=True,
+                      nt_stores=mode != "integrate_auto_traj_temporal")
     print("kernel_ms", eng.last_kernel_ms(), flush=True)
 '''
 
 
 def main():
     names = ["predict", "factor", "newton", "err", "diff", "grid", "select", "fail"]
-    for mode in ("mh_bdf", "integrate_auto_traj", "stiffmix"):
+    modes = sys.argv[1:] or ["mh_bdf", "integrate_auto_traj"]
+    for mode in modes:
         code = CHILD % {"root": ROOT, "tests": os.path.join(ROOT, "tests")}
         out = subprocess.run([sys.executable, "-c", code, mode], capture_output=True, text=True, timeout=300).stdout
+        if mode == "stiffmix2":
+            for l in out.splitlines():
+                if l.startswith("stiffmix2"):
+                    _, ms, rows = l.split(" ", 2)
+                    rows = json.loads(rows)
+                    print(json.dumps({"mode": mode, "kernel_ms": float(ms), "stiff_lanes": len(rows),
+                                      "slowest_8 [cycles_to_pass, cycles_in_pass, walker, wave]": rows[:8],
+                                      "median_cycles_to_pass": sorted(r[0] for r in rows)[len(rows) // 2],
+                                      "median_cycles_in_pass": sorted(r[1] for r in rows)[len(rows) // 2]}))
+            continue
         lines = [l for l in out.splitlines() if l.startswith("bdf_clocks")]
         kms = [float(l.split()[1]) for l in out.splitlines() if l.startswith("kernel_ms")]
         if not lines:
