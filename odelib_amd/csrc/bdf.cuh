@@ -250,9 +250,12 @@ __device__ __forceinline__ DTab<S> dtab_column() {
 #ifndef OE_BDF_CLOCKS
 #define OE_BDF_CLOCKS 0
 #endif
+#ifndef OE_LANE_CLOCKS  // the same for a lane's DOPRI5 step (lane.cuh, tools/lane_phases.py)
+#define OE_LANE_CLOCKS 0
+#endif
 enum BdfPhase { kPhPredict, kPhFactor, kPhNewton, kPhErr, kPhDiff, kPhGrid, kPhSelect, kPhFail, kPhN };
 struct BdfClk {
-#if OE_BDF_CLOCKS
+#if OE_BDF_CLOCKS || OE_LANE_CLOCKS
   uint64_t c[kPhN], last;
   uint32_t n[kPhN];
   __device__ __forceinline__ void start() {
@@ -472,9 +475,7 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
   int i = st.i, c;
   bool crossed = false;
   do {
-    c = 0;
-#pragma unroll
-    for (int j = 0; j < kWin; ++j) c += (st.wv[j] <= tn) ? 1 : 0;
+    c = dp::count_le(st.wv, tn);
     if (c == 0) break;
     crossed = true;
     // the next window goes straight into st.wv, loaded BEFORE this chunk's row stores (on

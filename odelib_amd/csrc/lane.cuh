@@ -108,6 +108,10 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
 #pragma unroll
   for (int s = 0; s < S; ++s) { cy[s] = y[s]; cydf[s] = 0.0; cbsp[s] = 0.0; cr4[s] = 0.0; cr5[s] = 0.0; }
 
+#if OE_LANE_CLOCKS  // measurement builds: s_memtime per phase of a lane's DOPRI5 step (bdf.cuh BdfClk)
+  BdfClk lclk;
+  lclk.start();
+#endif
   bool more = true;
   while (more) {  // one segment per observed grid index, then the rest of the grid (uniform)
     const bool is_obs = k < pb.n_obs;
@@ -144,6 +148,9 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
       for (int s = 0; s < S; ++s)
         yn[s] = fma(b76, k6[s], fma(b75, k5[s], fma(b74, k4[s], fma(b73, k3[s], fma(b71, k1[s], y[s])))));
       M::rhs(yn, t + h, p, k7);
+#if OE_LANE_CLOCKS
+      lclk.mark(0);
+#endif
       const double g1 = h * tb.v[20], g3 = h * tb.v[21], g4 = h * tb.v[22], g5 = h * tb.v[23], g6 = h * tb.v[24],
                    g7 = h * tb.v[25];
       double num = 0.0, den = 1.0, nfe = 0.0;
@@ -186,6 +193,9 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
       // the controller's safe·err^(-1/5), shared by the accept and reject paths (a wave whose
       // lanes split between them would otherwise run the root twice)
       const double sfe = safe * inv_fifth_root(err > 0.0 ? err : 1.0);
+#if OE_LANE_CLOCKS
+      lclk.mark(1);
+#endif
       if (!handed && err <= 1.0) {  // an accepted step (not handed over at its start)
         const double tn = last ? tend : t + h;
         if (tn >= t_seg) {  // the step that crosses the segment's time: keep its coefficients
@@ -203,18 +213,14 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
           rh_c = 1.0 / h;
         }
         // grid points in (t, tn]: counted on the window, which then moves past them
-        int c = 0;
-#pragma unroll
-        for (int j = 0; j < kGridWin; ++j) c += (wv[j] <= tn) ? 1 : 0;
+        int c = count_le(wv, tn);
         if (c != 0) {
           nst = 0;
           i += c;
           while (c == kGridWin) {  // more grid points than the window in one step
 #pragma unroll
             for (int j = 0; j < kGridWin; ++j) wv[j] = times[i + j];
-            c = 0;
-#pragma unroll
-            for (int j = 0; j < kGridWin; ++j) c += (wv[j] <= tn) ? 1 : 0;
+            c = count_le(wv, tn);
             i += c;
           }
 #pragma unroll
@@ -245,6 +251,9 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
           evicted = true;
         }
       }
+#if OE_LANE_CLOCKS
+      lclk.mark(2);
+#endif
     }
     // ---- the segment's observation, evaluated by the whole wave (uniform records) ----
     // Every lane runs it (full EXEC: the out-of-line log is called from uniform control
@@ -278,7 +287,15 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
       }
     }
     while (k < pb.n_obs && obs[k].tidx == tidx) ++k;  // uniform
+#if OE_LANE_CLOCKS
+    lclk.mark(3);
+#endif
   }
+#if OE_LANE_CLOCKS
+  if (active)
+    printf("lane_clocks lane %d stages %lu %u error %lu %u accept %lu %u segment %lu %u\n", (int)(off >> 3),
+           lclk.c[0], lclk.n[0], lclk.c[1], lclk.n[1], lclk.c[2], lclk.n[2], lclk.c[3], lclk.n[3]);
+#endif
   if (evicted) {
     a.status |= ST_MAXSTEP;
 #pragma unroll

@@ -471,6 +471,21 @@ __device__ __forceinline__ double select_r(int r, const double (&c)[N]) {
   return b2 ? m1 : m0;
 }
 
+// how many of the grid times w[0..N) are <= x, per lane: the running count made opaque after
+// each term (an empty asm on its VGPR), so the count is N compare + add-with-carry.  (Summed as
+// plain bools, the vectoriser packs the N predicates into a bit mask and the callers'
+// c != 0 / c == N tests become bit operations: ~2x the VALU, with hazard nops.)
+template <int N>
+__device__ __forceinline__ int count_le(const double (&w)[N], double x) {
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    c += (w[j] <= x) ? 1 : 0;
+    asm("" : "+v"(c));
+  }
+  return c;
+}
+
 // x^(-1/5) for finite x > 0 (the step controller's err^(-1/5) and HINIT's
 // (0.01/dm)^(1/5)).  Only exact scalings (frexp/ldexp) and IEEE mul/fma, so the host
 // restatement (oracle/rk_ref.c inv_fifth_root) reproduces it bit for bit — libm's and
