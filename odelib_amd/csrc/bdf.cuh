@@ -459,15 +459,23 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
   ++st.neq;
   st.fresh = false;
   const double tn = st.t + st.h;
+  // scipy's update D[q+2] = d − D[q+1], D[q+1] = d, D[j] += D[j+1] (j = q..0), one state at a
+  // time with all of its old rows read first: the LDS reads go out together instead of one
+  // read-add-write round trip per row (the chain carries the new D[j+1] in a register)
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    if constexpr (Q + 2 < kRows) st.D(Q + 2, s) = d[s] - st.D(Q + 1, s);
+    double od[Q + 2];
+#pragma unroll
+    for (int j = 0; j <= Q + 1; ++j) od[j] = st.D(j, s);
+    if constexpr (Q + 2 < kRows) st.D(Q + 2, s) = d[s] - od[Q + 1];
     st.D(Q + 1, s) = d[s];
+    double nx = d[s];
+#pragma unroll
+    for (int j = Q; j >= 0; --j) {
+      nx = od[j] + nx;
+      st.D(j, s) = nx;
+    }
   }
-#pragma unroll
-  for (int j = Q; j >= 0; --j)
-#pragma unroll
-    for (int s = 0; s < S; ++s) st.D(j, s) = st.D(j, s) + st.D(j + 1, s);
   ++st.nst;
   st.clk.mark(kPhDiff);
   // grid points in (t, tn]: counted on the window, a window's worth at a time; the rows
