@@ -966,7 +966,10 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
 
 }  // namespace oe
 namespace oe {
-constexpr int kGridWin = 8;  // the time grid buffer carries kGridWin + 1 +inf sentinels (lane.cuh)
+#ifndef OE_GRID_WIN  // measurement builds (tools/build_alt.sh): the per-lane DOPRI5's grid window
+#define OE_GRID_WIN 8
+#endif
+constexpr int kGridWin = OE_GRID_WIN;  // the time grid buffer carries kGridWin + 1 +inf sentinels (lane.cuh)
 }
 #include "stiff.cuh"
 #include "bdf.cuh"
