@@ -748,7 +748,7 @@ def extra_configs(args, R, T, P):
     # C2-stiffmix: the C2 draws with 0.1 % of the walkers made stiff (tau = 1e5, the I1
     # compartment relaxing 4e4x faster): 'dopri5' keeps them in the shared step, so their
     # waves crawl at the stability limit; 'auto' (the drop-in default, LSODA-like) hands
-    # them to the Rosenbrock method.
+    # them to BDF at their eviction points, a step size and an order per walker.
     # C3 at rk4_substeps=1 is within rtol 1e-6 / atol 1e-4 of tight odeint (SURVEY §8c's
     # 20-state RK4 tolerance; tests/test_gpu_parity.py::test_c3_rk4_bench_accuracy);
     # rk4_substeps=3 is within rtol = atol = 1e-6 (2 is not: 1.09 of that budget).

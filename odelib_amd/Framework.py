@@ -145,9 +145,10 @@ class ModelFramework:
         # engine options are keyword-only and never shadow a parameter / state name
         eng = {k: kwargs.pop(k) for k in list(kwargs) if k in _ENGINE_KW
                and k not in self._pnames and k not in self._snames}
-        # default 'auto': odeint's LSODA behaviour (non-stiff DOPRI5, stiff walkers by the
-        # Rosenbrock method); 'dopri5' for wide models or where the stiff methods are
-        # unavailable (engine.AUTO_DEFAULT_MAX_STATES)
+        # default 'auto': odeint's LSODA behaviour (non-stiff DOPRI5; a walker the stiffness
+        # test flags continues with BDF from that point, n_states <= 8, or is redone by the
+        # Rosenbrock method for wider models); 'dopri5' for wide models or where the stiff
+        # methods are unavailable (engine.AUTO_DEFAULT_MAX_STATES)
         self.method = eng.get("method", "auto")
         self._method_default = "method" not in eng
         self.rtol = float(eng.get("rtol", ODEINT_TOL))

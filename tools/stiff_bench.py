@@ -4,9 +4,10 @@ draws; --model chain<N> for the wider chains) with a fraction of the walkers mad
     python tools/stiff_bench.py --fracs 0 0.001 0.01 --taus 1e5 1e6
 
 'dopri5' keeps stiff walkers in the shared step (the wave crawls at the stability limit,
-or evicts them as MAXSTEP after max_steps per interval); 'auto' evicts them after 15
-stiff steps and redoes them with the Rosenbrock method; 'rosenbrock' integrates every
-walker with it.  One JSON line per (fraction, tau, mode).
+or evicts them as MAXSTEP after max_steps per interval); 'auto' hands them to BDF at
+their eviction points after 15 stiff steps (n_states <= 8; wider models: a Rosenbrock redo);
+'rosenbrock' integrates every walker with RODAS.  One JSON line per (fraction, tau, mode).
+--contiguous makes the stiff walkers walkers 0..n-1 (one wave's lanes).
 """
 import argparse
 import json
