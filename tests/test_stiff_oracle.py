@@ -1,6 +1,7 @@
 """Pin the stiff methods' C restatement (oracle/rk_ref.c: 'rosenbrock' = the stiffly
-accurate RODAS method, 'auto' = DOPRI5 + per-walker stiffness test + Rosenbrock restart — the
-kernels' algorithm) against the reference's algorithm on stiff draws:
+accurate RODAS method, 'auto' = DOPRI5 + per-walker stiffness test + BDF from the eviction
+point for n_states <= 8, a Rosenbrock restart for wider models — the kernels' algorithms,
+DESIGN.md §3.6) against the reference's algorithm on stiff draws:
 odeint's LSODA switches to BDF there (Framework.py:656), so the yardstick is a tight
 implicit solution (scipy Radau, rtol 1e-13) and the reference's own odeint."""
 import os
