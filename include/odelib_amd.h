@@ -132,8 +132,13 @@ enum {
                            faster); later calls reuse the choice (built-in models: every
                            context of the process on that device).  The first call synchronizes
                            the stream.  Overrides OE_PIPE*, OE_HALF_WAVES. */
-  OE_PIPE_XCD = 16384u  /* with OE_PIPE / OE_PIPE_4 / OE_PIPE_8: the piped kernel's workgroups dealt
+  OE_PIPE_XCD = 16384u, /* with OE_PIPE / OE_PIPE_4 / OE_PIPE_8: the piped kernel's workgroups dealt
                            to the XCDs in runs of 512 walkers (OE_KERNEL_PIPE*X) */
+  OE_NO_HANDQ = 32768u  /* oe_integrate, OE_METHOD_AUTO, built-in models with S <= 4, at most 16 walkers
+                           per CU: keep each handed walker's BDF pass in its DOPRI5 wave, after the wave's
+                           DOPRI5 pass, instead of the hand-over queue (a BDF kernel beside the DOPRI5
+                           kernel on a second stream of the context, taking handed walkers as they are
+                           handed over; same results).  Larger ensembles always run in-wave. */
 };
 
 /* RK4 trajectory kernels (oe_last_variant; all bitwise identical; OE_TUNE times those
@@ -272,7 +277,10 @@ int oe_problem_set(oe_ctx* ctx, const oe_problem* problem);
  *   traj   [T][S][W] full trajectory, or NULL  (the odeint [T,S] output, :656)
  *   chi    [W] or NULL   Σ_finite (O − log C)²/(2S²)   (stats.py:41), NaN if all masked
  *   ssres  [W] or NULL   Σ_nan-skipping (C − exp O)²     (stats.py:52)
- *   status [W] or NULL */
+ *   status [W] or NULL
+ * OE_METHOD_AUTO with S <= 8 also keeps an n_obs * W * 8-byte device scratch in the context
+ * (the BDF pass's deferred observations), allocated on first use and grown as W grows;
+ * OE_ERR_HIP if that allocation fails. */
 int oe_integrate(oe_ctx* ctx, int64_t n_walkers, const double* y0, const double* theta,
                  double* traj, double* chi, double* ssres, int32_t* status, uint32_t flags);
 

@@ -222,7 +222,7 @@ constexpr int kMhBlock = 256;  // threads per workgroup of every kernel with a B
 #ifndef OE_BDF_D_REGS  // measurement builds: the difference table in registers (tools/build_alt.sh)
 #define OE_BDF_D_REGS 0
 #endif
-template <int S>
+template <int S, int LD = kMhBlock>
 struct DTab {
 #if OE_BDF_D_REGS
   double v[bdfl::kRows * S];
@@ -230,16 +230,17 @@ struct DTab {
   __device__ __forceinline__ double operator()(int r, int s) const { return v[r * S + s]; }
 #else
   double* p;  // this lane's column (LDS: the address space is inferred after inlining)
-  __device__ __forceinline__ double& operator()(int r, int s) const { return p[(r * S + s) * kMhBlock]; }
+  __device__ __forceinline__ double& operator()(int r, int s) const { return p[(r * S + s) * LD]; }
 #endif
 };
-template <int S>
-__device__ __forceinline__ DTab<S> dtab_column() {
+// LD: columns of the table = threads of the workgroup (kMhBlock; 64 in k_bdf_hq)
+template <int S, int LD = kMhBlock>
+__device__ __forceinline__ DTab<S, LD> dtab_column() {
 #if OE_BDF_D_REGS
-  return DTab<S>{};
+  return DTab<S, LD>{};
 #else
-  __shared__ double tab[bdfl::kRows * S * kMhBlock];
-  return DTab<S>{tab + threadIdx.x};
+  __shared__ double tab[bdfl::kRows * S * LD];
+  return DTab<S, LD>{tab + threadIdx.x};
 #endif
 }
 
@@ -282,9 +283,9 @@ __device__ __forceinline__ uint64_t* bdf_clk_wave_start() {
 }
 #endif
 
-template <int S>
+template <int S, int LD = kMhBlock>
 struct BdfLane {
-  DTab<S> D;                 // backward differences (scipy's D), in LDS
+  DTab<S, LD> D;                 // backward differences (scipy's D), in LDS
   double lu[S][S], dinv[S];  // LU of I − c·J
   int piv[S];
   double t, h;               // this lane's time and step size
@@ -296,8 +297,8 @@ struct BdfLane {
 };
 
 // scipy's change_D at a compile-time order Q (bdf::change_D's operations)
-template <int S, int Q>
-__device__ __forceinline__ void bdfl_change_D(DTab<S>& D, double factor) {
+template <int S, int Q, int LD>
+__device__ __forceinline__ void bdfl_change_D(DTab<S, LD>& D, double factor) {
   using namespace bdfl;
   double r[Q + 1][Q + 1];
 #pragma unroll
@@ -330,8 +331,8 @@ __device__ __forceinline__ void bdfl_change_D(DTab<S>& D, double factor) {
   }
 }
 
-template <int S>
-__device__ __forceinline__ void bdfl_change_D(DTab<S>& D, int q, double factor) {
+template <int S, int LD>
+__device__ __forceinline__ void bdfl_change_D(DTab<S, LD>& D, int q, double factor) {
   switch (q) {
     case 1: bdfl_change_D<S, 1>(D, factor); break;
     case 2: bdfl_change_D<S, 2>(D, factor); break;
@@ -342,8 +343,8 @@ __device__ __forceinline__ void bdfl_change_D(DTab<S>& D, int q, double factor) 
 }
 
 // Phase A: predictor y_p = Σ_{j<=Q} D_j, ψ = Σ γ_j D_j / α_Q, c = h / α_Q
-template <int S, int Q>
-__device__ __forceinline__ void bdfl_predict(const BdfLane<S>& st, double (&yp)[S], double (&psi)[S], double& c) {
+template <int S, int Q, int LD>
+__device__ __forceinline__ void bdfl_predict(const BdfLane<S, LD>& st, double (&yp)[S], double (&psi)[S], double& c) {
   using namespace bdfl;
   constexpr double ia = ialpha(Q);
   c = st.h * ia;
@@ -362,8 +363,8 @@ __device__ __forceinline__ void bdfl_predict(const BdfLane<S>& st, double (&yp)[
 
 // LU factors of I − c·J(t, y): J column by column (one-tangent duals; each entry the same
 // bits as the S + 1-tangent evaluation), straight into the LU array
-template <class M, int PMAX>
-__device__ __forceinline__ void bdfl_factor(BdfLane<M::S>& st, double c, const double (&y)[M::S], double t,
+template <class M, int PMAX, int LD>
+__device__ __forceinline__ void bdfl_factor(BdfLane<M::S, LD>& st, double c, const double (&y)[M::S], double t,
                                             const double (&p)[PMAX]) {
   constexpr int S = M::S;
   using D1 = Dual<1>;
@@ -399,8 +400,8 @@ struct TrajCol {
 
 // the observations at grid index nxt (the lane's next observed one): finiteness, and each
 // record's sum C to the scratch (the chi / R² terms follow after the pass)
-template <int S>
-__device__ __forceinline__ void bdfl_observe(const DevProblem& pb, BdfLane<S>& st, const double (&yo)[S], const ObsCol& oc,
+template <int S, int LD>
+__device__ __forceinline__ void bdfl_observe(const DevProblem& pb, BdfLane<S, LD>& st, const double (&yo)[S], const ObsCol& oc,
                                              Acc& a) {
   check_finite(yo, a);
   const Obs* obs = pb.obs;
@@ -420,8 +421,8 @@ __device__ __forceinline__ void bdfl_observe(const DevProblem& pb, BdfLane<S>& s
 }
 
 // the backward-difference interpolant of the step just accepted (order Q, ending at tn) at ti
-template <int S, int Q>
-__device__ __forceinline__ void bdfl_interp(const BdfLane<S>& st, double tn, double ti, double (&yo)[S]) {
+template <int S, int Q, int LD>
+__device__ __forceinline__ void bdfl_interp(const BdfLane<S, LD>& st, double tn, double ti, double (&yo)[S]) {
   const double h = st.h;
   double prod = 1.0;
 #pragma unroll
@@ -438,8 +439,8 @@ __device__ __forceinline__ void bdfl_interp(const BdfLane<S>& st, double tn, dou
 
 // Phase C at order Q: error test; on acceptance the differences, the grid points of
 // (t, t + h] and — every Q + 1 equal steps — the order and step selection
-template <class M, int Q, bool TRAJ, bool NT>
-__device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S>& st, const double (&yn)[M::S],
+template <class M, int Q, bool TRAJ, bool NT, int LD>
+__device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S, LD>& st, const double (&yn)[M::S],
                                               const double (&d)[M::S], int niter, double (&y)[M::S], const ObsCol& oc,
                                               const TrajCol& tc, Acc& a) {
   using namespace bdfl;
@@ -570,8 +571,8 @@ __device__ __forceinline__ void bdfl_conclude(const DevProblem& pb, BdfLane<M::S
 }
 
 // One step attempt of a live lane (called in divergent control flow)
-template <class M, int PMAX, bool TRAJ, bool NT>
-__device__ __forceinline__ void bdfl_step(const DevProblem& pb, BdfLane<M::S>& st, const double (&p)[PMAX],
+template <class M, int PMAX, bool TRAJ, bool NT, int LD>
+__device__ __forceinline__ void bdfl_step(const DevProblem& pb, BdfLane<M::S, LD>& st, const double (&p)[PMAX],
                                           double (&y)[M::S], const ObsCol& oc, const TrajCol& tc, Acc& a) {
   using namespace bdfl;
   constexpr int S = M::S;
@@ -678,7 +679,7 @@ __device__ __forceinline__ void bdfl_step(const DevProblem& pb, BdfLane<M::S>& s
 // their own (t, y, grid index i, observation record k); y is the final state on return.
 // W lanes in the launch, this lane's column w (the trajectory rows, TRAJ, and the scratch of
 // deferred observations).
-template <class M, int PMAX, bool TRAJ, bool NT>
+template <class M, int PMAX, bool TRAJ, bool NT, int LD = kMhBlock>
 __device__ __forceinline__ void integrate_bdf_lane(const DevProblem& pb, double (&y)[M::S], double t, int i, int k,
                                                    const double (&p)[PMAX], double* traj, int64_t W, int64_t w,
                                                    bool active, bool part, Acc& a) {
@@ -691,8 +692,8 @@ __device__ __forceinline__ void integrate_bdf_lane(const DevProblem& pb, double 
   const ObsCol oc{pb.obs_c, W, w};
   const TrajCol tc{traj, W, w, active};
   const int k_first = k;
-  BdfLane<S> st;
-  st.D = dtab_column<S>();
+  BdfLane<S, LD> st;
+  st.D = dtab_column<S, LD>();
   st.live = part;
   st.t = t;
   st.i = i;

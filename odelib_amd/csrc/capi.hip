@@ -108,6 +108,16 @@ struct oe_ctx {
   void* obs_buf = nullptr;       // MH 'auto' / 'bdf' (S <= 8): the per-lane BDF pass's deferred
   size_t obs_bytes = 0;          // observations, [n_obs][lanes] (DevProblem::obs_c, bdf.cuh)
   int32_t last_mh_depth = 0;     // iterations per round of the last oe_mh_run (0: sequential)
+  // 'auto' integrate through the hand-over queue (ode_kernels.cuh HandQ): the BDF kernel's
+  // stream, the events ordering it between the queue's reset and the caller's stream, and the
+  // queue [(S + 5) doubles + 6 int32][cap] + 4 int32 of control
+  hipStream_t hq_stream = nullptr;
+  hipEvent_t ev_hq[2] = {nullptr, nullptr};
+  void* hq_buf = nullptr;
+  int64_t hq_cap = 0;
+  int32_t hq_S = 0;
+  int32_t hq_epoch = 0;
+  int32_t* hq_ctl = nullptr;  // the last launch's control words (ctl[3]: a BDF wave timed out)
   // OE_TUNE: the RK4 trajectory kernel chosen per shape, with what was measured (built-in
   // models: in a process-wide table shared by every context on the device; hipRTC models here)
   struct Tuned {
@@ -185,6 +195,36 @@ int ensure_obs_buf(oe_ctx* c, size_t bytes) {
   }
   OE_HIP(c, hipMalloc(&c->obs_buf, bytes));
   c->obs_bytes = bytes;
+  return OE_OK;
+}
+
+// the hand-over queue for W walkers of S states (zeroed: no slot carries a live epoch)
+int ensure_hq(oe_ctx* c, int64_t W, int S, HandQ* q) {
+  if (!c->hq_stream) {
+    OE_HIP(c, hipStreamCreateWithFlags(&c->hq_stream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) OE_HIP(c, hipEventCreateWithFlags(&c->ev_hq[k], hipEventDisableTiming));
+  }
+  const auto bytes = [](int64_t cap, int s) { return (size_t)cap * (8 * (size_t)(s + 5) + 4 * 6) + 64; };
+  if (c->hq_cap < W || c->hq_S < S) {
+    if (c->hq_buf) {
+      OE_HIP(c, hipStreamSynchronize(c->stream));
+      OE_HIP(c, hipStreamSynchronize(c->hq_stream));
+      OE_HIP(c, hipFree(c->hq_buf));
+      c->hq_buf = nullptr;
+      c->hq_cap = 0;
+    }
+    OE_HIP(c, hipMalloc(&c->hq_buf, bytes(W, S)));
+    OE_HIP(c, hipMemsetAsync(c->hq_buf, 0, bytes(W, S), c->stream));
+    c->hq_cap = W;
+    c->hq_S = S;
+  }
+  const int64_t cap = c->hq_cap;
+  q->d = static_cast<double*>(c->hq_buf);
+  q->n = reinterpret_cast<int32_t*>(q->d + (size_t)(c->hq_S + 5) * cap);
+  q->ctl = q->n + 6 * cap;
+  q->cap = (int32_t)cap;
+  if (++c->hq_epoch <= 0) c->hq_epoch = 1;  // (2^31 launches later: slots of long ago may match)
+  q->epoch = c->hq_epoch;
   return OE_OK;
 }
 
@@ -639,6 +679,13 @@ void oe_ctx_destroy(oe_ctx* c) {
     if (c->np_state) (void)hipFree(c->np_state);
     if (c->stiff_buf) (void)hipFree(c->stiff_buf);
     if (c->tree) (void)hipFree(c->tree);
+    if (c->hq_stream) {
+      (void)hipStreamSynchronize(c->hq_stream);
+      (void)hipStreamDestroy(c->hq_stream);
+    }
+    for (int k = 0; k < 2; ++k)
+      if (c->ev_hq[k]) (void)hipEventDestroy(c->ev_hq[k]);
+    if (c->hq_buf) (void)hipFree(c->hq_buf);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->np_stream) {
@@ -878,10 +925,13 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
   } else {
     ia.y0 = y0; ia.theta = theta; ia.traj = traj; ia.chi = chi; ia.ssres = ssres; ia.status = status;
   }
-  // the BDF pass ('auto' hand-over, 'bdf'; S <= 8) defers its observations to a
-  // [n_obs][W] scratch (bdf.cuh)
+  // the per-lane BDF pass ('auto' hand-over; S <= 8) defers its observations to a
+  // [n_obs][W] scratch (bdf.cuh).  Method 'bdf' runs the wave-lockstep pass here
+  // (bdf_wave.cuh), which observes in place (the per-lane one only in OE_LANE_INTEGRATE
+  // measurement builds without a trajectory).
   c->dp.obs_c = nullptr;
-  if ((c->method == OE_METHOD_AUTO || c->method == OE_METHOD_BDF) && S <= 8 && c->dp.n_obs > 0) {
+  const bool lane_bdf = c->method == OE_METHOD_AUTO || (OE_LANE_INTEGRATE && c->method == OE_METHOD_BDF && !traj);
+  if (lane_bdf && S <= 8 && c->dp.n_obs > 0) {
     rc = ensure_obs_buf(c, sizeof(double) * (size_t)c->dp.n_obs * (size_t)W);
     if (rc) return rc;
     c->dp.obs_c = static_cast<double*>(c->obs_buf);
@@ -914,6 +964,7 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     }
   }
   c->last_variant = variant;
+  c->hq_ctl = nullptr;
   const bool timing = !(flags & OE_NO_TIMING);
   if (timing) OE_HIP(c, hipEventRecord(c->ev0, c->stream));
   if (rk4_traj) {
@@ -958,8 +1009,36 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
       if (!ia.status) ia.status = c->stiff_buf + 64 + W;  // the marks need a status array
       sa.status = ia.status;
     }
-    if (!(wave_stiff && c->method == OE_METHOD_ROSENBROCK))
+    // 'auto', S <= kHandMaxS (built-in models): the hand-over queue — the DOPRI5 kernel on the
+    // caller's stream, the BDF kernel beside it on the context's second stream from the
+    // queue's reset on, the caller's stream waiting for both (ode_kernels.cuh HandQ)
+    const int tj = ia.traj ? 1 : 0, nj = nt ? 1 : 0;
+    // Only for small ensembles (<= 16 walkers per CU), where most SIMDs are free for the BDF
+    // waves: a BDF wave that shares its SIMD with a DOPRI5 wave slows it and is slowed by it.
+    // Measured (profiles/NOTES.md round 6, r06i; ms, in-wave -> queue, 0.1 % / 1 % stiff):
+    // 1 024 walkers 1.94 -> 1.54 / 2.96 -> 1.82; 4 096: 2.07 -> 1.75 / 3.14 -> 2.67; 16 384:
+    // 2.24 -> 2.17 / 3.08 -> 3.56; 65 536 (C2): 2.56 -> 2.71 / 2.82 -> 6.23.
+    const bool handq = c->method == OE_METHOD_AUTO && !e->rtc && e->integrate_hq[tj][nj] && !(flags & OE_NO_HANDQ) &&
+                       !OE_LANE_INTEGRATE && W <= (int64_t)OE_HQ_MAX_W_PER_CU * c->n_cu;
+    if (handq) {
+      HandQ q{};
+      rc = ensure_hq(c, W, S, &q);
+      if (rc) return rc;
+      q.n_waves = (int32_t)grid.x * (kBlock / 64);
+      OE_HIP(c, hipMemsetAsync(q.ctl, 0, 8 * sizeof(int32_t), c->stream));
+      OE_HIP(c, hipEventRecord(c->ev_hq[0], c->stream));
+      OE_HIP(c, hipStreamWaitEvent(c->hq_stream, c->ev_hq[0], 0));
+      e->integrate_hq[tj][nj](c->dp, ia, q, grid, block, c->stream);
+      OE_HIP(c, hipGetLastError());
+      e->bdf_hq[tj][nj](c->dp, ia, q, dim3((unsigned)std::min<int64_t>(kHandBdfWaves, 4 * (int64_t)c->n_cu)),
+                        dim3(64), c->hq_stream);
+      OE_HIP(c, hipGetLastError());
+      OE_HIP(c, hipEventRecord(c->ev_hq[1], c->hq_stream));
+      OE_HIP(c, hipStreamWaitEvent(c->stream, c->ev_hq[1], 0));
+      c->hq_ctl = q.ctl;
+    } else if (!(wave_stiff && c->method == OE_METHOD_ROSENBROCK)) {
       OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));
+    }
     if (wave_stiff) {
       const dim3 wgrid((unsigned)std::min<int64_t>(W, (int64_t)16 * c->n_cu)), wblock(64);
       if (c->method == OE_METHOD_AUTO) {
@@ -988,6 +1067,13 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     OE_HIP(c, hipStreamSynchronize(c->stream));
   } else if (!(flags & OE_ASYNC)) {
     OE_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  // synchronous calls through the hand-over queue: a BDF wave that gave up waiting (a slot
+  // never published within kHandTimeout: a bug, reported rather than hung on)
+  if (c->hq_ctl && (host || !(flags & OE_ASYNC))) {
+    int32_t timed_out = 0;
+    OE_HIP(c, hipMemcpy(&timed_out, c->hq_ctl + 3, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (timed_out) return fail(c, OE_ERR_HIP, "oe_integrate: the hand-over queue's BDF kernel timed out");
   }
   return OE_OK;
 }
@@ -1077,7 +1163,14 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   int depth = 0;
   const bool has_tree = split ? e->mh_split_tree != nullptr
                        : e->rtc ? e->rtc->mh_tree[c->method] != nullptr : e->mh_tree[c->method] != nullptr;
+  // the stiff methods of the register-path models have no iteration-loop kernel (kMhRoundsOnly):
+  // their chains always run in rounds, one iteration a round at the least
+  const bool rounds_only = !split && has_tree && (e->rtc ? e->rtc->mh[c->method] : (const void*)e->mh[c->method]) == nullptr;
   const int lanes_per_walker = split ? e->split_lanes : 1;
+  // bytes per tree lane: the node's proposal, chi, R² residual, status, and for the per-lane
+  // BDF pass ('auto' / 'bdf', S <= 8) its deferred observations (DevProblem::obs_c)
+  const bool lane_bdf = !split && (c->method == OE_METHOD_AUTO || c->method == OE_METHOD_BDF) && S <= 8;
+  const double lane_bytes = 8.0 * (P + 2) + 4.0 + (lane_bdf ? 8.0 * c->dp.n_obs : 0.0);
   if (a->speculate != 0 && has_tree && a->nits > 1) {
     const int64_t target = (int64_t)64 * 4 * c->n_cu / lanes_per_walker;
     if (a->speculate < 0) {
@@ -1089,9 +1182,10 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
     if (depth < 2 || ((int64_t(1) << depth) - 1) * W > kMaxWalkers) depth = 0;
     // the tree buffer ((2^d - 1)·W·(P + 2) doubles) within 4 GiB, like the draw buffers'
     // budget: a deeper explicit request is cut to the deepest tree that fits
-    while (depth >= 2 && (double)((int64_t(1) << depth) - 1) * (double)W * (8.0 * (P + 2) + 4.0) > 4294967296.0) --depth;
+    while (depth >= 2 && (double)((int64_t(1) << depth) - 1) * (double)W * lane_bytes > 4294967296.0) --depth;
     if (depth < 2) depth = 0;
   }
+  if (rounds_only && depth == 0) depth = 1;
   c->last_mh_depth = depth;
   MHTreeArgs ta{};
   if (depth) {
@@ -1108,6 +1202,7 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
       if (hipMalloc(&c->tree, bytes) != hipSuccess) {  // out of memory: one iteration per step
         (void)hipGetLastError();
         c->tree = nullptr;
+        if (rounds_only) return fail(c, OE_ERR_NOMEM, "oe_mh_run: no device memory for the MH round buffer");
         depth = 0;
         c->last_mh_depth = 0;
       } else {
@@ -1118,9 +1213,15 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
   // the per-lane BDF pass (MH 'auto' / 'bdf', one lane per chain, S <= 8) defers its
   // observations to a [n_obs][lanes] scratch: one column per lane of the largest launch
   c->dp.obs_c = nullptr;
-  if (!split && (c->method == OE_METHOD_AUTO || c->method == OE_METHOD_BDF) && S <= 8 && c->dp.n_obs > 0) {
+  if (lane_bdf && c->dp.n_obs > 0) {
     const int64_t lanes = depth ? ((int64_t(1) << depth) - 1) * W : W;
     rc = ensure_obs_buf(c, sizeof(double) * (size_t)c->dp.n_obs * (size_t)lanes);
+    if (rc && depth >= 2) {  // out of memory for a speculative tree's scratch: one iteration a round
+      (void)hipGetLastError();
+      depth = rounds_only ? 1 : 0;
+      c->last_mh_depth = depth;
+      rc = ensure_obs_buf(c, sizeof(double) * (size_t)c->dp.n_obs * (size_t)W);
+    }
     if (rc) return rc;
     c->dp.obs_c = static_cast<double*>(c->obs_buf);
   }

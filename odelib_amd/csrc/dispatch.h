@@ -18,6 +18,7 @@ using IntegrateLaunch = void (*)(const DevProblem&, const IntegrateArgs&, dim3, 
 using MHLaunch = void (*)(const DevProblem&, const MHArgs&, dim3, dim3, hipStream_t);
 using StiffWaveLaunch = void (*)(const DevProblem&, const StiffWaveArgs&, dim3, dim3, hipStream_t);
 using MHTreeLaunch = void (*)(const DevProblem&, const MHTreeArgs&, dim3, dim3, hipStream_t);
+using HandQLaunch = void (*)(const DevProblem&, const IntegrateArgs&, const HandQ&, dim3, dim3, hipStream_t);
 
 struct Entry {
   int32_t model_id;
@@ -28,7 +29,12 @@ struct Entry {
   IntegrateLaunch integrate[kMethods][2][2];
   IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > OE_PIPE_MAX_S
   IntegrateLaunch dopri5_piped[2];  // [nt]: DOPRI5 trajectories through store waves; null when S > 6
+  // 'auto' through the hand-over queue, [traj][nt] (S <= kHandMaxS): the DOPRI5 kernel and the
+  // BDF kernel beside it
+  HandQLaunch integrate_hq[2][2];
+  HandQLaunch bdf_hq[2][2];
   MHLaunch mh[kMethods];
+  MHLaunch mh_init[kMethods];  // the a-priori pass (MHArgs::init)
   MHTreeLaunch mh_tree[kMethods];  // speculative MH rounds (k_mh_tree); the resolve kernel is shared
   StiffWaveLaunch stiff_wave[2][2];  // [traj][nt]: S > kStiffRegS stiff redo, one wave per walker
   IntegrateLaunch dopri5_split[2][2];  // [traj][nt]: DOPRI5 with split_lanes lanes per walker (split.cuh)
@@ -56,9 +62,10 @@ inline hipError_t launch_mh_entry(const Entry* e, int method, const DevProblem& 
     DevProblem a0 = dp;
     MHArgs a1 = ma;
     void* args[] = {(void*)&a0, (void*)&a1};
-    return hipModuleLaunchKernel(e->rtc->mh[method], g.x, g.y, g.z, b.x, b.y, b.z, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(ma.init ? e->rtc->mh_init[method] : e->rtc->mh[method], g.x, g.y, g.z, b.x, b.y, b.z,
+                                 0, s, args, nullptr);
   }
-  e->mh[method](dp, ma, g, b, s);
+  (ma.init ? e->mh_init : e->mh)[method](dp, ma, g, b, s);
   return hipGetLastError();
 }
 
@@ -74,9 +81,17 @@ template <class M, bool NT>
 void launch_dopri5_piped(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_integrate_dopri5_piped<M, NT>), g, b, 0, s, pb, ia);
 }
-template <class M, int METHOD>
+template <class M, bool TRAJ, bool NT>
+void launch_integrate_hq(const DevProblem& pb, const IntegrateArgs& ia, const HandQ& q, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_integrate_hq<M, TRAJ, NT>), g, b, 0, s, pb, ia, q);
+}
+template <class M, bool TRAJ, bool NT>
+void launch_bdf_hq(const DevProblem& pb, const IntegrateArgs& ia, const HandQ& q, dim3 g, dim3 b, hipStream_t s) {
+  hipLaunchKernelGGL((k_bdf_hq<M, TRAJ, NT>), g, b, 0, s, pb, ia, q);
+}
+template <class M, int METHOD, bool INIT = false>
 void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
-  hipLaunchKernelGGL((k_mh<M, METHOD>), g, b, 0, s, pb, ma);
+  hipLaunchKernelGGL((k_mh<M, METHOD, INIT>), g, b, 0, s, pb, ma);
 }
 inline hipError_t launch_mh_tree_entry(const Entry* e, int method, const DevProblem& dp, const MHTreeArgs& ta,
                                        dim3 g, dim3 b, hipStream_t s) {
@@ -137,7 +152,10 @@ void fill_method(Entry& e) {
   e.integrate[METHOD][0][1] = launch_integrate<M, METHOD, false, false>;  // NT only matters with a trajectory
   e.integrate[METHOD][1][0] = launch_integrate<M, METHOD, true, false>;
   e.integrate[METHOD][1][1] = launch_integrate<M, METHOD, true, true>;
-  e.mh[METHOD] = launch_mh<M, METHOD>;
+  // the stiff methods' MH chains with one lane per chain (S <= kStiffRegS) run as rounds of
+  // k_mh_tree + k_mh_resolve, one iteration a round when not speculating (kMhRoundsOnly)
+  if constexpr (!kMhRoundsOnly<M, METHOD>) e.mh[METHOD] = launch_mh<M, METHOD>;
+  e.mh_init[METHOD] = launch_mh<M, METHOD, true>;
   e.mh_tree[METHOD] = launch_mh_tree<M, METHOD>;
 }
 
@@ -154,6 +172,14 @@ Entry make_entry(int32_t model_id) {
     fill_method<M, kRosenbrock>(e);
   }
   if constexpr (M::S <= kStiffRegS) fill_method<M, kBdf>(e);
+  if constexpr (M::S <= kHandMaxS) {
+    e.integrate_hq[0][0] = e.integrate_hq[0][1] = launch_integrate_hq<M, false, false>;
+    e.integrate_hq[1][0] = launch_integrate_hq<M, true, false>;
+    e.integrate_hq[1][1] = launch_integrate_hq<M, true, true>;
+    e.bdf_hq[0][0] = e.bdf_hq[0][1] = launch_bdf_hq<M, false, false>;
+    e.bdf_hq[1][0] = launch_bdf_hq<M, true, false>;
+    e.bdf_hq[1][1] = launch_bdf_hq<M, true, true>;
+  }
   if constexpr (M::S <= 8 && dp_pipe_slots<M::S>() >= 2) {  // a slot ring of >= 2 steps fits (S <= 6)
     e.dopri5_piped[0] = launch_dopri5_piped<M, false>;
     e.dopri5_piped[1] = launch_dopri5_piped<M, true>;

@@ -29,6 +29,15 @@
 // counted on a window of kGridWin grid times loaded one step ahead.
 #pragma once
 
+#ifndef OE_LANE_TAB_VREG
+#define OE_LANE_TAB_VREG false
+#endif
+#ifndef OE_LANE_TAB_PIN  // the tableau's SGPR immediates defined at each integration's start (load_tab PIN)
+#define OE_LANE_TAB_PIN true
+#endif
+#ifndef OE_LANE_AUTO_TAB  // 'auto' lanes: 0 tableau immediates, 1 in VGPRs, 2 mixed (load_tab MIX)
+#define OE_LANE_AUTO_TAB 1
+#endif
 namespace oe {
 
 
@@ -56,7 +65,7 @@ __device__ __forceinline__ void integrate_dopri5_lane(const DevProblem& pb, doub
   const double tend = times[pb.T - 1];
   const double rtol = pb.rtol, atol = pb.atol;
   double t = t0;
-  const Tab tb = load_tab<false>();
+  const Tab tb = load_tab<OE_LANE_TAB_VREG || (AUTO && OE_LANE_AUTO_TAB > 0), AUTO && OE_LANE_AUTO_TAB == 2, OE_LANE_TAB_PIN>();
   double k1[S], k2[S], k3[S], k4[S], k5[S], k6[S], k7[S], yt[S], yn[S];
   M::rhs(y, t, p, k1);
 

@@ -220,8 +220,16 @@ __device__ __forceinline__ void st_row(__amdgpu_buffer_rsrc_t rsrc, uint32_t lan
 // materialised per call (a call per observation / proposal, not per step).  A callee
 // starts with s_waitcnt vmcnt(0), which drains the trajectory stores in flight, so the
 // RK4 trajectory kernel (67 VGPRs either way) keeps the inline log (observe<S, true>).
+#ifndef OE_TRANSC_CALL
+#define OE_TRANSC_CALL 1
+#endif
+#if OE_TRANSC_CALL
 __device__ __attribute__((noinline)) double oe_log(double x) { return log(x); }
 __device__ __attribute__((noinline)) double oe_exp(double x) { return exp(x); }
+#else
+__device__ __forceinline__ double oe_log(double x) { return log(x); }
+__device__ __forceinline__ double oe_exp(double x) { return exp(x); }
+#endif
 
 // NaN-propagating finiteness accumulator: a.nf becomes NaN iff some y[s] is NaN/inf.
 template <int S>
@@ -434,10 +442,16 @@ constexpr double safe = 0.9, facmin = 0.2, facmax = 10.0;
 __device__ const double kTab[36] = {a21, a31, a32, a41, a42, a43, a51, a52, a53, a54, a61, a62, a63, a64, a65,
                                     a71, a73, a74, a75, a76, e1, e3, e4, e5, e6, e7, d1, d3, d4, d5, d6, d7,
                                     c2, c3, c4, c5};
+constexpr double kTabC[36] = {a21, a31, a32, a41, a42, a43, a51, a52, a53, a54, a61, a62, a63, a64, a65,
+                              a71, a73, a74, a75, a76, e1, e3, e4, e5, e6, e7, d1, d3, d4, d5, d6, d7,
+                              c2, c3, c4, c5};
 struct Tab {
   double v[36];
 };
-template <bool VREG>
+// MIX (with VREG; k_integrate_hq): the stage couplings a_ij in VGPRs, the error, dense-output
+// and node coefficients (e, d, c: 16 of 36) as immediates — 32 VGPRs fewer, for the
+// co-residency budget of the hand-over queue's DOPRI5 kernel.
+template <bool VREG, bool MIX = false, bool PIN = false>
 __device__ __forceinline__ Tab load_tab() {
   Tab t;
   if constexpr (VREG) {
@@ -445,13 +459,29 @@ __device__ __forceinline__ Tab load_tab() {
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // opaque per-lane zero: vector loads, values stay in VGPRs
     const double* p = kTab + z;
 #pragma unroll
-    for (int j = 0; j < 36; ++j) t.v[j] = p[j];
+    for (int j = 0; j < 36; ++j) t.v[j] = (MIX && j >= 20) ? kTabC[j] : p[j];
   } else {
     const double c[36] = {a21, a31, a32, a41, a42, a43, a51, a52, a53, a54, a61, a62, a63, a64, a65,
                           a71, a73, a74, a75, a76, e1, e3, e4, e5, e6, e7, d1, d3, d4, d5, d6, d7,
                           c2, c3, c4, c5};
 #pragma unroll
-    for (int j = 0; j < 36; ++j) t.v[j] = c[j];
+    for (int j = 0; j < 36; ++j) {
+      if constexpr (PIN) {
+        // SGPR immediates materialised here, at the integration's start (two s_mov inside a
+        // volatile asm), instead of hoisted into the kernel's prologue: in the MH kernels they
+        // would live across the whole iteration loop (proposal, accept, every call site),
+        // where they are spilled to VGPR lanes
+        constexpr uint64_t kOne = 1;
+        const uint64_t b = __builtin_bit_cast(uint64_t, c[j]);
+        uint32_t lo, hi;
+        asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3" : "=s"(lo), "=s"(hi)
+                     : "i"((uint32_t)(b & 0xffffffffu)), "i"((uint32_t)(b >> 32)));
+        (void)kOne;
+        t.v[j] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+      } else {
+        t.v[j] = c[j];
+      }
+    }
   }
   return t;
 }
@@ -603,19 +633,102 @@ __device__ __forceinline__ void dp_pipe_publish(DpPipe<S>& pp, double t, double 
   if (pp.lane == 0) *pp.produced = pp.n;
 }
 
+// ---- The hand-over queue of 'auto' (S <= kHandMaxS, small ensembles: k_integrate_hq / k_bdf_hq) ----
+// In k_integrate<M, auto> a lane handed to BDF waits for its wave's whole DOPRI5 pass and then
+// runs its BDF pass in that wave: the wave's time is its DOPRI5 pass plus its slowest handed
+// lane's BDF pass.  The queue splits LSODA's two halves over two kernels that run at the same
+// time on two streams: k_integrate_hq (the lockstep DOPRI5 pass without the BDF code, ~200
+// registers) puts a handed walker's state into a device-memory slot at its eviction point, and
+// k_bdf_hq (one-wave workgroups at ~310 registers: 200 + 312 <= 512, so they sit beside the
+// DOPRI5 waves) takes the slots as they fill, one walker per wave while they fit, and runs the
+// per-lane BDF pass (bdf.cuh).  A per-lane BDF pass does not depend on the lane or wave running
+// it (profiles/NOTES.md r05o): the same bits.  It pays only where the DOPRI5 waves leave SIMDs
+// free — a BDF wave sharing a SIMD with a DOPRI5 wave slows it and is slowed by it — so
+// oe_integrate takes it up to OE_HQ_MAX_W_PER_CU walkers per CU (NOTES round 6: 1 024 walkers
+// with 0.1 % / 1 % stiff 1.94 -> 1.54 / 2.96 -> 1.82 ms; C2's 65 536: 2.56 -> 2.71 / 2.82 ->
+// 6.23, hence in-wave there).  An in-kernel version (BDF waves in the DOPRI5 workgroups) had to
+// fit every wave in 256 registers and its BDF steps ran ~1.5x slower.
+// Protocol (device scope): a producer lane reserves slot j (atomic ctl[0]), writes its state,
+// and publishes ready[j] = epoch with a release store; each producer wave adds one to ctl[2]
+// after its pass.  A BDF wave claims a run of reserved slots (CAS on ctl[1]), waits for their
+// ready flags and leaves once every producer wave is counted and no reserved slot is unclaimed.
+// Producers never wait on the BDF kernel, so any schedule of the two kernels finishes (run one
+// after the other, the queue is simply full when BDF starts); a BDF wave also leaves, flagging
+// ctl[3], past kHandTimeout.
+constexpr int kHandMaxS = 4;  // the co-residency budget above (S = 5..8 keep the in-wave pass)
+#ifndef OE_HQ_MAX_W_PER_CU  // oe_integrate takes the queue up to this many walkers per CU (r06i:
+#define OE_HQ_MAX_W_PER_CU 16  // W = 1 024 / 4 096 win 20-40 %, 16 384 mixed, 65 536 loses)
+#endif
+#ifndef OE_HQ_POLL  // measurement builds: s_sleep(127)s between two polls of the queue
+#define OE_HQ_POLL 8
+#endif
+#ifndef OE_HQ_MIX  // measurement builds: 0 = every tableau coefficient in VGPRs (breaks the budget)
+#define OE_HQ_MIX 1
+#endif
+#ifndef OE_HQ_WAVES  // measurement builds: one-wave workgroups of k_bdf_hq (capped at 4 per CU)
+#define OE_HQ_WAVES 1024
+#endif
+#ifndef OE_HQ_PRIO  // measurement builds: 0 = the BDF waves at the default priority
+#define OE_HQ_PRIO 1
+#endif
+#ifndef OE_HQ_TRACE  // measurement builds: a handed walker's chi / R² outputs carry, in µs from the
+#define OE_HQ_TRACE 0  // DOPRI5 kernel's first wave, its BDF wave's start and (claim·1e5 + BDF pass)
+#endif
+constexpr uint64_t kHandTimeout = 6000000000ull;  // s_memrealtime ticks (100 MHz): 60 s
+struct HandQ {
+  double* d;        // [(S + 5)][cap]: y[0..S), t, chi, ssres, nf, ymin
+  int32_t* n;       // [6][cap]: i, k, nvalid, status, walker, ready
+  int32_t* ctl;     // [0] reserved, [1] claimed, [2] producer waves done, [3] timeout
+  int32_t cap;      // slots (>= walkers of the launch)
+  int32_t epoch;    // ready[j] == epoch: slot j of this launch is published
+  int32_t n_waves;  // producer waves of the launch
+};
+// Polls are relaxed device-scope loads: an acquire load at agent scope invalidates the XCD's L2
+// on every poll, and a few hundred polling waves then cost the DOPRI5 kernel 3x its time
+// (r06c).  One acquire fence follows a successful poll (the slot data, the final count).
+__device__ __forceinline__ int32_t hq_load(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void hq_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+// a producer lane's hand-over: its state at the eviction point (y, t, grid index i, next
+// observation record k, accumulators; status gets ST_STIFF as the BDF pass's input)
+template <int S>
+__device__ __forceinline__ void hand_push(const HandQ& q, const double (&y)[S], double t, int i, int k,
+                                          const Acc& a, int64_t w) {
+  const int64_t c = q.cap;
+  const int j = atomicAdd(q.ctl, 1);
+#pragma unroll
+  for (int s = 0; s < S; ++s) q.d[s * c + j] = y[s];
+  q.d[S * c + j] = t;
+  q.d[(S + 1) * c + j] = a.chi;
+  q.d[(S + 2) * c + j] = a.ssres;
+  q.d[(S + 3) * c + j] = a.nf;
+  q.d[(S + 4) * c + j] = a.ymin;
+  q.n[j] = i;
+  q.n[c + j] = k;
+  q.n[2 * c + j] = a.nvalid;
+  q.n[3 * c + j] = a.status | ST_STIFF;
+  q.n[4 * c + j] = (int32_t)w;
+  __hip_atomic_store(q.n + 5 * c + j, q.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // RESUME (auto, S <= kStiffRegS): an evicted lane is handed over to BDF — its state at the
 // eviction point goes to *rs and the return value says so — instead of being redone from t0.
+// QUEUE (with RESUME, k_integrate_hq): it goes to the hand-over queue *hq instead, and the lane
+// stores no more rows (the BDF kernel writes them).
 // PIPE (trajectory mode, S <= 8, k_integrate_dopri5_piped): the rows go through *pp to the
 // store wave (same values, same minimum), the compute wave only evaluates observed rows.
 template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false, bool SLOW_REDO = false, bool RESUME = false,
-          bool PIPE = false>
+          bool PIPE = false, bool QUEUE = false>
 __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, uint32_t off, bool active, Acc& a,
-                                                 Resume<M::S>* rs = nullptr, DpPipe<M::S>* pp = nullptr) {
+                                                 Resume<M::S>* rs = nullptr, DpPipe<M::S>* pp = nullptr,
+                                                 const HandQ* hq = nullptr) {
   using namespace dp;
   constexpr int S = M::S;
   static_assert(!PIPE || (TRAJ && S <= 8 && !AUTO), "the piped output is DOPRI5 trajectory mode's, S <= 8");
+  static_assert(!QUEUE || RESUME, "the hand-over queue takes the RESUME hand-over");
   int k = 0;
   if constexpr (PIPE) {  // row 0 = the initial state: a slot whose end time is times[0]
     const double t00 = kconst(pb.times)[0];
@@ -631,7 +744,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
   bool dead = !active;  // dead lanes never enter the wave norm
   bool handed = false;  // RESUME: this lane was handed over to BDF
   double t = t0;
-  const Tab tb = load_tab<TRAJ && (M::S <= 8)>();
+  const Tab tb = load_tab<TRAJ && (M::S <= 8), QUEUE && OE_HQ_MIX>();
   double k1[S], k2[S], k3[S], k4[S], k5[S], k6[S], k7[S], yt[S], yn[S];
   M::rhs(y, t, p, k1);
 
@@ -784,7 +897,10 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
         }
         if (!dead && n_stiff >= 15) {  // hand the walker to the stiff method
           dead = true;
-          if constexpr (RESUME) {  // at the start of this step
+          if constexpr (QUEUE) {  // at the start of this step, to the BDF kernel
+            handed = true;
+            hand_push<S>(*hq, y, t, i, k, a, (int64_t)(off >> 3));
+          } else if constexpr (RESUME) {  // at the start of this step
             handed = true;
 #pragma unroll
             for (int s = 0; s < S; ++s) rs->y[s] = y[s];
@@ -845,7 +961,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
             for (int s = 0; s < S; ++s)
               yo[s] = fma(th, fma(th1, fma(th, fma(th1, r5[s], r4[s]), bsp[s]), ydf[s]), y[s]);
             // (an evicted lane's state is NaN, so its dense output is NaN already)
-            if constexpr (!PIPE) store_row_at<S, TRAJ, NT>(trow, yo, W, off, active, a);
+            if constexpr (!PIPE) store_row_at<S, TRAJ, NT>(trow, yo, W, off, QUEUE ? active && !handed : active, a);
             if (i == nxt) {
               observe_next<S>(pb, i, yo, k, nxt, a);
               t_obs = times[nxt < pb.T ? nxt : pb.T];
@@ -858,7 +974,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
         if (t_i == tn) {  // a grid point on the step's end
           t_i = *tnext++;
           if (kAll || i == nxt) {
-            if constexpr (!PIPE) store_row_at<S, TRAJ, NT>(trow, yn, W, off, active, a);
+            if constexpr (!PIPE) store_row_at<S, TRAJ, NT>(trow, yn, W, off, QUEUE ? active && !handed : active, a);
             if (i == nxt) {
               observe_next<S>(pb, i, yn, k, nxt, a);
               t_obs = times[nxt < pb.T ? nxt : pb.T];
@@ -920,7 +1036,10 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
     if (i < pb.T && (nst >= pb.max_steps || h < hmin)) {  // (not after the last grid point)
       if (!dead && el >= 0.5 * err) {
         dead = true;
-        if constexpr (RESUME) {  // handed over at its current state
+        if constexpr (QUEUE) {  // handed over at its current state, to the BDF kernel
+          handed = true;
+          hand_push<S>(*hq, y, t, i, k, a, (int64_t)(off >> 3));
+        } else if constexpr (RESUME) {  // handed over at its current state
           handed = true;
 #pragma unroll
           for (int s = 0; s < S; ++s) rs->y[s] = y[s];
@@ -1139,6 +1258,154 @@ __global__ void __launch_bounds__(256)
     if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
     if (ia.ssres) ia.ssres[w] = a.ssres;
     if (ia.status) ia.status[w] = finish(a);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Kernels 1d/1e: 'auto' (S <= kHandMaxS) as two concurrent kernels over the hand-over
+// queue (HandQ above).  k_integrate_hq is k_integrate<M, auto>'s lockstep DOPRI5 pass with
+// the queue in place of the in-wave BDF pass; k_bdf_hq, launched at the same time on a second
+// stream, runs the per-lane BDF pass of each handed walker from its hand-over state.
+// Together: k_integrate<M, auto, TRAJ, NT>'s outputs, bit for bit.
+// ---------------------------------------------------------------------------------
+template <class M, bool TRAJ, bool NT>
+__global__ void __launch_bounds__(256) k_integrate_hq(const DevProblem pb, const IntegrateArgs ia, const HandQ hq) {
+  constexpr int S = M::S;
+  constexpr int PMAX = kPmax<M>;
+  static_assert(S <= kHandMaxS, "the hand-over queue's co-residency budget");
+#if OE_HQ_TRACE
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store((uint64_t*)(hq.ctl + 4), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+#endif
+  const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x, ia.xcd_remap) : (int64_t)blockIdx.x;
+  const int64_t gw = blk * blockDim.x + threadIdx.x;
+  const bool active = gw < ia.W;
+  const int64_t w = active ? gw : ia.W - 1;  // tail lanes shadow the last walker, never store
+  const int64_t W = ia.W;
+  double y[S], p[PMAX];
+#pragma unroll
+  for (int s = 0; s < S; ++s) y[s] = ia.y0[(int64_t)s * W + w];
+#pragma unroll
+  for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
+  Acc a = acc_init();
+  const bool handed = integrate_dopri5<M, PMAX, TRAJ, NT, true, false, true, false, true>(
+      pb, y, p, ia.traj, W, (uint32_t)w * 8u, active, a, nullptr, nullptr, &hq);
+  if (active && !handed) {
+    if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
+    if (ia.ssres) ia.ssres[w] = a.ssres;
+    if (ia.status) ia.status[w] = finish(a);
+  }
+#if OE_HQ_TRACE
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_max((uint64_t*)(hq.ctl + 6), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+#endif
+  // this wave's pass is over (its slots were published, each with its own release store; the
+  // count only ends the BDF kernel's polling, so it needs no release — a release here writes
+  // the XCD's L2 back, once per wave)
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(hq.ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kHandBdfWaves = OE_HQ_WAVES;  // k_bdf_hq workgroups (one wave each): 4 per CU, one per SIMD
+template <class M, bool TRAJ, bool NT>
+__global__ void __launch_bounds__(64) k_bdf_hq(const DevProblem pb, const IntegrateArgs ia, const HandQ hq) {
+  constexpr int S = M::S;
+  constexpr int PMAX = kPmax<M>;
+  const int lane = (int)threadIdx.x;
+  const int64_t W = ia.W, c = hq.cap;
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    // lane 0 claims a run of reserved slots
+    int base = -1, m = 0;
+    if (lane == 0) {
+      for (;;) {
+        const int done = hq_load(hq.ctl + 2);
+        const int r = hq_load(hq.ctl);
+        int cl = hq_load(hq.ctl + 1);
+        if (r > cl) {
+          // one walker per BDF wave while the pending ones fit the kernel's waves: a lone lane
+          // runs the pass fastest (a wave's batch waits for its slowest walker); beyond that,
+          // the backlog shared out
+          const int want = min(64, max(1, (r - cl) / (int)gridDim.x));
+          if (__hip_atomic_compare_exchange_strong(hq.ctl + 1, &cl, cl + want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            base = cl;
+            m = want;
+            break;
+          }
+          continue;
+        }
+        if (done >= hq.n_waves) {  // every producer wave counted: `reserved` is final
+          hq_acquire();
+          if (hq_load(hq.ctl) <= hq_load(hq.ctl + 1)) break;
+          continue;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t_start > kHandTimeout) {
+          __hip_atomic_store(hq.ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        // ~OE_HQ_POLL x 8 000 cycles between polls: a few hundred pollers must not load the
+        // queue's control line (or the memory side behind it) the DOPRI5 kernel also uses
+        for (int z = 0; z < OE_HQ_POLL; ++z) __builtin_amdgcn_s_sleep(127);
+      }
+    }
+    base = __shfl(base, 0);
+    m = __shfl(m, 0);
+    if (base < 0) break;
+    const bool part = lane < m;
+    const int j = base + (part ? lane : 0);
+    // a claimed slot is reserved: its producer lane is writing it
+    bool late = false;
+    for (;;) {
+      const bool ok = !part || hq_load(hq.n + 5 * c + j) == hq.epoch;
+      if (__ballot(!ok) == 0ull) break;
+      if (__builtin_amdgcn_s_memrealtime() - t_start > kHandTimeout) {
+        late = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (late) {
+      if (lane == 0) __hip_atomic_store(hq.ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    hq_acquire();  // the slots' data, published by their producers' release stores
+    double y[S], p[PMAX];
+#pragma unroll
+    for (int s = 0; s < S; ++s) y[s] = hq.d[s * c + j];
+    const double t = hq.d[S * c + j];
+    Acc a{hq.d[(S + 1) * c + j], hq.d[(S + 2) * c + j], hq.d[(S + 3) * c + j], hq.d[(S + 4) * c + j],
+          hq.n[2 * c + j], hq.n[3 * c + j]};
+    const int i = hq.n[j], k = hq.n[c + j];
+    const int64_t w = hq.n[4 * c + j];
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) p[q] = (q < pb.P) ? ia.theta[(int64_t)q * W + w] : 0.0;
+#if OE_HQ_TRACE
+    const uint64_t t_claim = __builtin_amdgcn_s_memrealtime();
+#endif
+    // The BDF pass is one lane's dependency chain (latency-bound, sparse issue); the DOPRI5
+    // wave sharing its SIMD is issue-bound.  At a higher priority the BDF wave issues whenever
+    // it is ready, taking few slots from the DOPRI5 wave, instead of waiting behind it.
+    if (OE_HQ_PRIO) __builtin_amdgcn_s_setprio(3);
+    integrate_bdf_lane<M, PMAX, TRAJ, NT, 64>(pb, y, t, i, k, p, ia.traj, W, w, part, part, a);
+    if (OE_HQ_PRIO) __builtin_amdgcn_s_setprio(0);
+#if OE_HQ_TRACE
+    {
+      const uint64_t t0 = __hip_atomic_load((const uint64_t*)(hq.ctl + 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // s_memrealtime: 100 MHz; chi = start·1e5 + the DOPRI5 kernel's last wave end, ssres =
+      // claim·1e5 + BDF pass, all in whole µs from the DOPRI5 kernel's first wave
+      const uint64_t t_pend = __hip_atomic_load((const uint64_t*)(hq.ctl + 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.chi = (double)((int64_t)(t_start - t0) / 100) * 1e5 + (double)((int64_t)(t_pend - t0) / 100);
+      a.ssres = (double)((int64_t)(t_claim - t0) / 100) * 1e5 + (double)((__builtin_amdgcn_s_memrealtime() - t_claim) / 100);
+      a.nvalid = 1;
+    }
+#endif
+    if (part) {
+      if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
+      if (ia.ssres) ia.ssres[w] = a.ssres;
+      if (ia.status) ia.status[w] = finish(a);
+    }
   }
 }
 
@@ -1506,13 +1773,38 @@ __device__ __forceinline__ T* opaque(T* p) {
   asm volatile("" : "+s"(p));
   return p;
 }
+// The same for a wave-uniform scalar (a kernel argument): the predicates the MH iteration
+// derives from it — j < P, walk bit j, init_param[s] == j per state and parameter (the
+// '<state>0' picks) — are formed at their use in each iteration instead of hoisted out of
+// the iteration loop as 64-bit lane masks, ~50 of which lived across the whole integration
+// in SGPR pairs spilled to VGPR lanes (k_mh<TwoI, auto>: 510 SGPRs spilled).
+#ifndef OE_MH_W_OPAQUE
+#define OE_MH_W_OPAQUE 0
+#endif
+template <class T>
+__device__ __forceinline__ T uopaque(T v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
 
 // The stiff methods' Rosenbrock fallback (dual-number Jacobian, in-register LU) would set
 // the register budget of the whole MH kernel (chain5 'auto': 300 VGPR+AGPR, one wave per
 // SIMD, +49 % per iteration at 262 144 walkers); for S = 5, where the plain DOPRI5 MH
 // kernel runs two waves per SIMD, asking for two keeps the DOPRI5 phase there (80 B of
 // scratch, in the rare path).  S = 6..8 DOPRI5 MH kernels are at one wave per SIMD anyway.
+// The stiff methods' MH with one lane per chain (S <= kStiffRegS) has no iteration-loop kernel:
+// its chains run as rounds of k_mh_tree + k_mh_resolve (below), of one iteration when not
+// speculating.  k_mh's loop around the per-lane DOPRI5 + BDF passes held ~160-380 SGPRs
+// spilled to VGPR lanes (the regime of round 4's unexplained code-shape failures; DESIGN.md
+// §3.6), where the loop-free tree kernel holds ~20; a round costs two launches.
 template <class M, int METHOD>
+constexpr bool kMhRoundsOnly = (METHOD == kAuto || METHOD == kBdf) && M::S <= kStiffRegS;
+
+// INIT: the a-priori fit's pass alone (ma.init, Samplers.py:88-91) — its own kernel, so k_mh's
+// iteration loop is the kernel's only copy of the integrator (with the init branch inside
+// k_mh, the two copies of a stiff method's BDF pass shared one register allocation: ~100 of
+// k_mh<TwoI, auto>'s spilled SGPRs held values across both).
+template <class M, int METHOD, bool INIT = false>
 __global__ void __launch_bounds__(256)
     __attribute__((amdgpu_waves_per_eu((METHOD == kRosenbrock && M::S == 5) ? 2 : 1)))
     k_mh(const DevProblem pb, const MHArgs ma) {
@@ -1524,7 +1816,7 @@ __global__ void __launch_bounds__(256)
   const int64_t gw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = gw < ma.W;
   const int64_t w = active ? gw : ma.W - 1;
-  const int64_t W = ma.W;
+  const int64_t W0 = ma.W;
   const int P = pb.P;
   // The chain state θ [P][W] and y0 [S][W] stays in HBM between iterations (a few loads
   // per iteration against ~1000 integration steps): only the proposal is held in
@@ -1534,7 +1826,8 @@ __global__ void __launch_bounds__(256)
   double* __restrict__ y0g = ma.y0;
   const uint32_t off = (uint32_t)w * 8u;  // W <= 2^29 (oe_mh_run)
 
-  if (ma.init) {  // a-priori fit (Samplers.py:88-91)
+  if constexpr (INIT) {  // a-priori fit (Samplers.py:88-91)
+    const int64_t W = W0;
     double th[PMAX], y[S];
 #pragma unroll
     for (int j = 0; j < PMAX; ++j) th[j] = (j < P) ? Row(theta + (int64_t)j * W, W).ld(off) : 0.0;
@@ -1550,9 +1843,7 @@ __global__ void __launch_bounds__(256)
       Row(ma.cur + 3 * W, W).st(off, 0.0);
       if (ma.status) ma.status[w] = finish(a);
     }
-    return;
-  }
-
+  } else {
   // The current chain point (chi, R², AIC, acceptance count; status) also stays in
   // HBM (cur rows): read after the proposal's integration, written on accept, so none
   // of it holds registers across the integration.
@@ -1560,22 +1851,36 @@ __global__ void __launch_bounds__(256)
   const int PS = P + 5;
 
   for (int it = ma.it0; it < ma.it1; ++it) {
+    // (W re-read per iteration: the row offsets j·W·8 are formed at their use, not hoisted
+    // into the kernel's prologue and kept across the whole loop)
+    int64_t W = OE_MH_W_OPAQUE ? uopaque(W0) : W0;
     // ---- proposal: θ' = exp(log θ + N(0, sd)) for walking parameters (Framework.py:107-122)
     double tn[PMAX];
     theta = opaque(theta);
     y0g = opaque(y0g);
     const double* dz = opaque(ma.dz + (int64_t)(it - ma.draw_it0) * P * W);
+    {
+      // one call site each for log and exp: a loop over the parameters, the result put in
+      // place with selects.  Unrolled, every call site is a point where the caller-saved
+      // SGPRs live across the call are spilled to VGPR lanes and restored — 2·PMAX of them.
+      const int Pu = uopaque(P);
+      const uint64_t wm = uopaque(ma.walk_mask);
 #pragma unroll
-    for (int j = 0; j < PMAX; ++j) {
-      const double thj = (j < P) ? Row(theta + (int64_t)j * W, W).ld(off) : 0.0;
-      tn[j] = (j < P && ((ma.walk_mask >> j) & 1ull)) ? oe_exp(oe_log(thj) + Row(dz + (int64_t)j * W, W).ld(off)) : thj;
+      for (int j = 0; j < PMAX; ++j) tn[j] = 0.0;
+#pragma unroll 1
+      for (int j = 0; j < Pu; ++j) {
+        const double thj = Row(theta + (int64_t)j * W, W).ld(off);
+        const double v = ((wm >> j) & 1ull) ? oe_exp(oe_log(thj) + Row(dz + (int64_t)j * W, W).ld(off)) : thj;
+#pragma unroll
+        for (int q = 0; q < PMAX; ++q) tn[q] = (q == j) ? v : tn[q];
+      }
     }
     // '<state>0' parameters drive initial states (Samplers.py:110-114)
     double y[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const int pi = ma.init_param[s];
-      y[s] = (ma.any_walk && pi >= 0) ? pick(tn, pi) : Row(y0g + (int64_t)s * W, W).ld(off);
+      const int pi = uopaque(ma.init_param[s]);
+      y[s] = (uopaque(ma.any_walk) && pi >= 0) ? pick(tn, pi) : Row(y0g + (int64_t)s * W, W).ld(off);
     }
     // ---- integrate + fused chi (Samplers.py:115-116)
     Acc a = acc_init();
@@ -1584,6 +1889,7 @@ __global__ void __launch_bounds__(256)
     theta = opaque(theta);
     y0g = opaque(y0g);
     cur = opaque(cur);
+    if (OE_MH_W_OPAQUE) W = uopaque(W0);
 #if OE_MH_CHECKS
     // Integrity of the wave-uniform state every store below depends on:
     // the row pointers carried through the integration (live in SGPRs or spilled across
@@ -1610,6 +1916,7 @@ __global__ void __launch_bounds__(256)
     const double lr = oe_exp(chi - chin);
     const double accp = oe_exp(oe_log(lr));
     const bool acc = accp > u;
+    const int Pa = uopaque(P);
     if (acc) {
       chi = chin;
       rsq = 1.0 - a.ssres / pb.sstot;
@@ -1618,7 +1925,7 @@ __global__ void __launch_bounds__(256)
       if (active) {
 #pragma unroll
         for (int j = 0; j < PMAX; ++j)
-          if (j < P) Row(theta + (int64_t)j * W, W).st(off, tn[j]);
+          if (j < Pa) Row(theta + (int64_t)j * W, W).st(off, tn[j]);
         Row(cur, W).st(off, chi);
         Row(cur + W, W).st(off, rsq);
         Row(cur + 2 * W, W).st(off, aic);
@@ -1628,10 +1935,10 @@ __global__ void __launch_bounds__(256)
     }
     // linked initial states follow the current parameters: the accepted proposal, or
     // on reject the restored ones (Samplers.py:110-114, :137-143)
-    if (ma.any_walk && active) {
+    if (uopaque(ma.any_walk) && active) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        const int pi = ma.init_param[s];
+        const int pi = uopaque(ma.init_param[s]);
         if (pi >= 0) Row(y0g + (int64_t)s * W, W).st(off, acc ? pick(tn, pi) : Row(theta + (int64_t)pi * W, W).ld(off));
       }
     }
@@ -1640,13 +1947,14 @@ __global__ void __launch_bounds__(256)
       double* row = ma.samples + (int64_t)(it - ma.row0) * PS * W;
 #pragma unroll
       for (int j = 0; j < PMAX; ++j)
-        if (j < P) Row(row + (int64_t)j * W, W).st(off, acc ? tn[j] : Row(theta + (int64_t)j * W, W).ld(off));
+        if (j < Pa) Row(row + (int64_t)j * W, W).st(off, acc ? tn[j] : Row(theta + (int64_t)j * W, W).ld(off));
       Row(row + (int64_t)P * W, W).st(off, chi);
       Row(row + (int64_t)(P + 1) * W, W).st(off, rsq);
       Row(row + (int64_t)(P + 2) * W, W).st(off, aic);
       Row(row + (int64_t)(P + 3) * W, W).st(off, (double)it);
       Row(row + (int64_t)(P + 4) * W, W).st(off, nacc / (double)it);
     }
+  }
   }
 }
 

@@ -15,6 +15,7 @@ struct RtcModule {
   hipModule_t stiff_mod = nullptr;        // auto + Rosenbrock + BDF (+ k_stiff_wave)
   hipFunction_t integrate[5][2][2] = {};  // [method][traj][nt]; the stiff methods null until built
   hipFunction_t mh[5] = {};
+  hipFunction_t mh_init[5] = {};           // the a-priori pass (k_mh<.., INIT = true>)
   hipFunction_t mh_tree[5] = {};          // speculative MH rounds (k_mh_tree)
   hipFunction_t stiff_wave[2][2] = {};    // [traj][nt]: S > kStiffRegS with the stiff methods
   int stiff = 0;                          // 0: not built yet, 1: built, -1: unavailable (stiff_err)

@@ -29,6 +29,9 @@ std::string rtc_integrate_name(int method, int traj, int nt) {
   return std::string("oe::k_integrate<UserModel, ") + kMethodName[method] + ", " + kBool[traj] + ", " + kBool[nt] + ">";
 }
 std::string rtc_mh_name(int method) { return std::string("oe::k_mh<UserModel, ") + kMethodName[method] + ">"; }
+std::string rtc_mh_init_name(int method) {
+  return std::string("oe::k_mh<UserModel, ") + kMethodName[method] + ", true>";
+}
 std::string rtc_mh_tree_name(int method) {
   return std::string("oe::k_mh_tree<UserModel, ") + kMethodName[method] + ">";
 }
@@ -36,6 +39,9 @@ std::string rtc_stiff_wave_name(int traj, int nt) {
   return std::string("oe::k_stiff_wave<UserModel, ") + kBool[traj] + ", " + kBool[nt] + ">";
 }
 static bool has_stiff_wave(int S, RtcPart part) { return part == kRtcStiff && S > kStiffRegS; }
+// k_mh's iteration loop for method m (ode_kernels.cuh kMhRoundsOnly: the stiff methods of
+// register-path models run their chains as k_mh_tree rounds only)
+static bool has_mh_loop(int S, int m) { return !((m == 2 || m == 4) && S <= kStiffRegS); }
 static int first_method(RtcPart part) { return part == kRtcStiff ? 2 : 0; }
 // the methods of a part: RK4 + DOPRI5; auto + Rosenbrock (+ BDF up to kStiffRegS states)
 static int end_method(int S, RtcPart part) { return part == kRtcStiff ? (S <= kStiffRegS ? 5 : 4) : 2; }
@@ -56,7 +62,8 @@ std::string rtc_source(const std::string& body, int S, int P, RtcPart part) {
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt)
         src += "template __global__ void " + rtc_integrate_name(m, tr, nt) + "(const oe::DevProblem, const oe::IntegrateArgs);\n";
-    src += "template __global__ void " + rtc_mh_name(m) + "(const oe::DevProblem, const oe::MHArgs);\n";
+    if (has_mh_loop(S, m)) src += "template __global__ void " + rtc_mh_name(m) + "(const oe::DevProblem, const oe::MHArgs);\n";
+    src += "template __global__ void " + rtc_mh_init_name(m) + "(const oe::DevProblem, const oe::MHArgs);\n";
     src += "template __global__ void " + rtc_mh_tree_name(m) + "(const oe::DevProblem, const oe::MHTreeArgs);\n";
   }
   if (has_stiff_wave(S, part))
@@ -110,7 +117,9 @@ static std::vector<std::string> all_names(int S, RtcPart part) {
   for (int m = m0; m < end_method(S, part); ++m)
     for (int tr = 0; tr < 2; ++tr)
       for (int nt = 0; nt < 2; ++nt) names.push_back(rtc_integrate_name(m, tr, nt));
-  for (int m = m0; m < end_method(S, part); ++m) names.push_back(rtc_mh_name(m));
+  for (int m = m0; m < end_method(S, part); ++m)
+    if (has_mh_loop(S, m)) names.push_back(rtc_mh_name(m));
+  for (int m = m0; m < end_method(S, part); ++m) names.push_back(rtc_mh_init_name(m));
   for (int m = m0; m < end_method(S, part); ++m) names.push_back(rtc_mh_tree_name(m));
   if (has_stiff_wave(S, part))
     for (int tr = 0; tr < 2; ++tr)
@@ -155,7 +164,9 @@ int rtc_build(const std::string& body, int S, int P, const char* arch, RtcPart p
       for (int nt = 0; nt < 2; ++nt)
         if (!get(&out->integrate[m][tr][nt])) return -1;
   for (int m = m0; m < end_method(S, part); ++m)
-    if (!get(&out->mh[m])) return -1;
+    if (has_mh_loop(S, m) && !get(&out->mh[m])) return -1;
+  for (int m = m0; m < end_method(S, part); ++m)
+    if (!get(&out->mh_init[m])) return -1;
   for (int m = m0; m < end_method(S, part); ++m)
     if (!get(&out->mh_tree[m])) return -1;
   if (has_stiff_wave(S, part))

@@ -20,6 +20,10 @@ Draws (two_i, the notebook's 4-state model):
 Stored (numbers only): theta, trajectories [W][T][S] (states before summation), the
 predictions at the observations, chi, R², AIC, per tolerance.
 
+LSODA's step / RHS / Jacobian counts on the same stiff draws and the MH starts below
+(lsoda_counts.json; ``--lsoda-counts`` writes only these): odeint's ``full_output`` info of
+the reference's own integrate call.
+
 Metropolis–Hastings chains in the stiff region (mh_stiff.npz + mh_stiff.json): the
 reference's own ``Statistics.Samplers.MetropolisHastings`` (Samplers.py:53-174: LSODA for
 every proposal, Framework.py:656; its global numpy stream seeded with random_seed) from the
@@ -116,12 +120,58 @@ def mh_chains(ODElib):
     print("stiff MH chains written:", meta)
 
 
+def lsoda_counts(ODElib):
+    """LSODA's own work on the stiff draws and the stiff MH starts (lsoda_counts.json): the
+    reference's ``ModelFramework.integrate`` with its ``odeint`` name rebound to a wrapper that
+    makes the same call with ``full_output=True`` and keeps the info dict (Framework.py:656;
+    nothing else of the call changes, the wrapper returns the trajectory the reference gets).
+    Per draw: steps (nst), RHS evaluations (nfe), Jacobian evaluations (nje), the output
+    points LSODA reached on BDF (mused == 2) and the first such time — the cost model the
+    device's DOPRI5 + BDF hand-over is compared against (tests/test_stiff_oracle.py)."""
+    import json
+    from scipy.integrate import odeint
+    fw = sys.modules["ODElib.Framework"]
+    saved = fw.odeint
+    info = {}
+
+    def wrapped(*a, **k):
+        y, d = odeint(*a, full_output=True, **k)
+        info.update(d)
+        return y
+
+    rows = {}
+    st, labels = stiff_thetas()
+    draws = [(lab, list(st[w])) for w, lab in enumerate(labels)]
+    draws += [(key, [th[p] for p in ("mu", "phi", "beta", "lam", "tau")]) for key, th, _, _ in MH_STIFF]
+    m = build_model(ODElib, "two_i")
+    fw.odeint = wrapped
+    try:
+        for lab, ps in draws:
+            info.clear()
+            m.integrate(parameters=(ps,), as_dataframe=False, sum_subpopulations=False)
+            mused = np.asarray(info["mused"])
+            tcur = np.asarray(info["tcur"])
+            bdf = np.nonzero(mused == 2)[0]
+            rows[lab] = dict(theta=[float(v) for v in ps], nst=int(info["nst"][-1]), nfe=int(info["nfe"][-1]),
+                             nje=int(info["nje"][-1]), bdf_outputs=int(bdf.size), outputs=int(mused.size),
+                             first_bdf_t=float(tcur[bdf[0]]) if bdf.size else None)
+    finally:
+        fw.odeint = saved
+    with open(os.path.join(HERE, "lsoda_counts.json"), "w") as f:
+        json.dump(rows, f, indent=1, sort_keys=True)
+    print("LSODA counts written:", rows)
+
+
 def main():
     ODElib = import_reference()
     warnings.filterwarnings("ignore")
     if "--mh-only" in sys.argv:
         mh_chains(ODElib)
         return
+    if "--lsoda-counts" in sys.argv:
+        lsoda_counts(ODElib)
+        return
+    lsoda_counts(ODElib)
     mh_chains(ODElib)
     m = build_model(ODElib, "two_i")
     out = {}

@@ -319,3 +319,33 @@ def test_bdf_handover_in_a_lockstep_group_matches_tight_solution():
     for w in list(lanes) + [0, 63]:
         ref = _radau(fp, y0[:, w], theta[:, w])
         np.testing.assert_allclose(out["traj"][:, :, w], ref, rtol=1e-6, atol=1e-6, err_msg=str(w))
+
+
+def test_step_counts_against_lsoda_on_the_reference_draws():
+    """the device's DOPRI5 + BDF hand-over against odeint's LSODA on the stiff
+    draws and the stiff MH starts of the golden set (tests/golden/lsoda_counts.json: LSODA's
+    own nst / nfe / nje from the reference's integrate call, Framework.py:656).  Steps are the
+    stiff workload's cost model; no draw may take more than 1.5x LSODA's steps (a regression
+    in the hand-over or the BDF controller shows here first).  Prints the table
+    (profiles/NOTES.md round 6)."""
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "lsoda_counts.json")) as f:
+        lsoda = json.load(f)
+    m = product_model("two_i", method="auto")
+    fp = m.fit_problem()
+    y0 = np.asarray(m.get_inits(), float)[:, None].copy()
+    rows = []
+    for lab, ref in sorted(lsoda.items()):
+        rk_ref.dopri5_stats(); rk_ref.bdf_stats(); rk_ref.bdf_detail()
+        out = rk_ref.integrate(fp, y0, np.asarray(ref["theta"], float)[:, None].copy(), trajectory=False, lane=True)
+        dp, bs, bd = rk_ref.dopri5_stats(), rk_ref.bdf_stats(), rk_ref.bdf_detail()
+        dsteps = dp["accepted"] + dp["rejected"]
+        rhs = 3 + 6 * dsteps + ((2 + bd["newton_iterations"] + 4 * bs["jacobians"]) if bs["steps"] else 0)
+        steps = dsteps + bs["steps"]
+        rows.append((lab, steps, dsteps, bs["steps"], rhs, bs["jacobians"], ref["nst"], ref["nfe"], ref["nje"]))
+        assert out["status"][0] & 8, lab  # every one of them is handed to BDF, as LSODA switches
+        assert steps <= 1.5 * ref["nst"], (lab, steps, ref["nst"])
+    print("\n%-20s %6s %7s %5s %6s %4s | %6s %6s %4s" % ("draw", "steps", "dopri5", "bdf", "rhs", "jac", "nst",
+                                                         "nfe", "nje"))
+    for r in rows:
+        print("%-20s %6d %7d %5d %6d %4d | %6d %6d %4d" % r)
