@@ -132,13 +132,8 @@ enum {
                            faster); later calls reuse the choice (built-in models: every
                            context of the process on that device).  The first call synchronizes
                            the stream.  Overrides OE_PIPE*, OE_HALF_WAVES. */
-  OE_PIPE_XCD = 16384u, /* with OE_PIPE / OE_PIPE_4 / OE_PIPE_8: the piped kernel's workgroups dealt
+  OE_PIPE_XCD = 16384u  /* with OE_PIPE / OE_PIPE_4 / OE_PIPE_8: the piped kernel's workgroups dealt
                            to the XCDs in runs of 512 walkers (OE_KERNEL_PIPE*X) */
-  OE_NO_HANDQ = 32768u  /* oe_integrate, OE_METHOD_AUTO, built-in models with S <= 4, at most 16 walkers
-                           per CU: keep each handed walker's BDF pass in its DOPRI5 wave, after the wave's
-                           DOPRI5 pass, instead of the hand-over queue (a BDF kernel beside the DOPRI5
-                           kernel on a second stream of the context, taking handed walkers as they are
-                           handed over; same results).  Larger ensembles always run in-wave. */
 };
 
 /* RK4 trajectory kernels (oe_last_variant; all bitwise identical; OE_TUNE times those

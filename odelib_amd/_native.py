@@ -24,7 +24,7 @@ OE_MODEL_ZERO_I, OE_MODEL_ONE_I, OE_MODEL_TWO_I, OE_MODEL_CHAIN = 0, 1, 2, 3
 OE_MODEL_CUSTOM = 1000
 OE_STATUS_NONFINITE, OE_STATUS_NEGATIVE, OE_STATUS_MAXSTEP, OE_STATUS_STIFF, OE_STATUS_INTERNAL = 1, 2, 4, 8, 16
 OE_HOST_PTRS, OE_ASYNC, OE_NT_STORES, OE_PIPE, OE_HALF_WAVES, OE_NO_XCD_REMAP, OE_NO_TIMING = 1, 2, 4, 8, 16, 64, 128
-OE_PIPE_4, OE_PIPE_8, OE_XCD_RANGES, OE_NO_SPLIT, OE_TUNE, OE_PIPE_XCD, OE_NO_HANDQ = 512, 1024, 2048, 4096, 8192, 16384, 32768
+OE_PIPE_4, OE_PIPE_8, OE_XCD_RANGES, OE_NO_SPLIT, OE_TUNE, OE_PIPE_XCD = 512, 1024, 2048, 4096, 8192, 16384
 OE_KERNEL_DIRECT, OE_KERNEL_HALF, OE_KERNEL_PIPE2, OE_KERNEL_PIPE4, OE_KERNEL_PIPE8 = range(5)
 OE_KERNEL_PIPE2X, OE_KERNEL_PIPE4X, OE_KERNEL_PIPE8X, OE_KERNEL_OTHER = range(5, 9)
 OE_KERNEL_COUNT = 9

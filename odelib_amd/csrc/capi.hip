@@ -110,7 +110,7 @@ struct oe_ctx {
   int32_t last_mh_depth = 0;     // iterations per round of the last oe_mh_run (0: sequential)
   // 'auto' integrate through the hand-over queue (ode_kernels.cuh HandQ): the BDF kernel's
   // stream, the events ordering it between the queue's reset and the caller's stream, and the
-  // queue [(S + 5) doubles + 6 int32][cap] + 4 int32 of control
+  // queue [(S + 5) doubles + 6 int32][cap] + 16 int32 of control
   hipStream_t hq_stream = nullptr;
   hipEvent_t ev_hq[2] = {nullptr, nullptr};
   void* hq_buf = nullptr;
@@ -798,7 +798,8 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
         }
       }
       if (cm->rtc.stiff != 1) return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: " + cm->rtc.stiff_err);
-    } else if (e->integrate[p->method][0][0] == nullptr) {
+    } else if (e->integrate[p->method][0][0] == nullptr &&
+               !(p->method == OE_METHOD_AUTO && e->integrate_hq[0][0] != nullptr)) {
       return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: the stiff methods (auto, rosenbrock) need n_states <= " +
                                              std::to_string(kStiffMaxS));
     }
@@ -1009,32 +1010,36 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
       if (!ia.status) ia.status = c->stiff_buf + 64 + W;  // the marks need a status array
       sa.status = ia.status;
     }
-    // 'auto', S <= kHandMaxS (built-in models): the hand-over queue — the DOPRI5 kernel on the
-    // caller's stream, the BDF kernel beside it on the context's second stream from the
-    // queue's reset on, the caller's stream waiting for both (ode_kernels.cuh HandQ)
+    // 'auto', S <= kHandMaxS (built-in models): the hand-over queue (ode_kernels.cuh HandQ) —
+    // the DOPRI5 kernel on the caller's stream; the BDF kernel beside it on the context's
+    // second stream for small ensembles (<= OE_HQ_MAX_W_PER_CU walkers per CU), else after it
+    // on the same stream; the caller's stream waits for both
     const int tj = ia.traj ? 1 : 0, nj = nt ? 1 : 0;
-    // Only for small ensembles (<= 16 walkers per CU), where most SIMDs are free for the BDF
-    // waves: a BDF wave that shares its SIMD with a DOPRI5 wave slows it and is slowed by it.
-    // Measured (profiles/NOTES.md round 6, r06i; ms, in-wave -> queue, 0.1 % / 1 % stiff):
-    // 1 024 walkers 1.94 -> 1.54 / 2.96 -> 1.82; 4 096: 2.07 -> 1.75 / 3.14 -> 2.67; 16 384:
-    // 2.24 -> 2.17 / 3.08 -> 3.56; 65 536 (C2): 2.56 -> 2.71 / 2.82 -> 6.23.
-    const bool handq = c->method == OE_METHOD_AUTO && !e->rtc && e->integrate_hq[tj][nj] && !(flags & OE_NO_HANDQ) &&
-                       !OE_LANE_INTEGRATE && W <= (int64_t)OE_HQ_MAX_W_PER_CU * c->n_cu;
+    const bool handq = c->method == OE_METHOD_AUTO && !e->rtc && e->integrate_hq[tj][nj] && !OE_LANE_INTEGRATE;
+    const bool beside = W <= (int64_t)OE_HQ_MAX_W_PER_CU * c->n_cu;  // else: after the DOPRI5 kernel
     if (handq) {
       HandQ q{};
       rc = ensure_hq(c, W, S, &q);
       if (rc) return rc;
       q.n_waves = (int32_t)grid.x * (kBlock / 64);
-      OE_HIP(c, hipMemsetAsync(q.ctl, 0, 8 * sizeof(int32_t), c->stream));
-      OE_HIP(c, hipEventRecord(c->ev_hq[0], c->stream));
-      OE_HIP(c, hipStreamWaitEvent(c->hq_stream, c->ev_hq[0], 0));
+      OE_HIP(c, hipMemsetAsync(q.ctl, 0, 10 * sizeof(int32_t), c->stream));
+      hipStream_t bs = c->stream;
+      if (beside) {
+        OE_HIP(c, hipEventRecord(c->ev_hq[0], c->stream));
+        OE_HIP(c, hipStreamWaitEvent(c->hq_stream, c->ev_hq[0], 0));
+        bs = c->hq_stream;
+      }
       e->integrate_hq[tj][nj](c->dp, ia, q, grid, block, c->stream);
       OE_HIP(c, hipGetLastError());
-      e->bdf_hq[tj][nj](c->dp, ia, q, dim3((unsigned)std::min<int64_t>(kHandBdfWaves, 4 * (int64_t)c->n_cu)),
-                        dim3(64), c->hq_stream);
+      // one wave per walker (slots dealt statically, k_bdf_hq): beside the DOPRI5 kernel up to
+      // kHandBdfWaves, after it one wave per SIMD (a round of dispatch when nothing was handed)
+      const int64_t G = std::min<int64_t>(beside ? (int64_t)kHandBdfWaves : 4 * (int64_t)c->n_cu, W);
+      e->bdf_hq[tj][nj](c->dp, ia, q, dim3((unsigned)G), dim3(64), bs);
       OE_HIP(c, hipGetLastError());
-      OE_HIP(c, hipEventRecord(c->ev_hq[1], c->hq_stream));
-      OE_HIP(c, hipStreamWaitEvent(c->stream, c->ev_hq[1], 0));
+      if (beside) {
+        OE_HIP(c, hipEventRecord(c->ev_hq[1], c->hq_stream));
+        OE_HIP(c, hipStreamWaitEvent(c->stream, c->ev_hq[1], 0));
+      }
       c->hq_ctl = q.ctl;
     } else if (!(wave_stiff && c->method == OE_METHOD_ROSENBROCK)) {
       OE_HIP(c, launch_integrate_entry(e, c->method, ia.traj ? 1 : 0, nt ? 1 : 0, c->dp, ia, grid, block, c->stream));

@@ -148,10 +148,13 @@ struct SplitOf<TwoI> { static constexpr int K = OE_SPLIT_TWOI; };
 
 template <class M, int METHOD>
 void fill_method(Entry& e) {
-  e.integrate[METHOD][0][0] = launch_integrate<M, METHOD, false, false>;
-  e.integrate[METHOD][0][1] = launch_integrate<M, METHOD, false, false>;  // NT only matters with a trajectory
-  e.integrate[METHOD][1][0] = launch_integrate<M, METHOD, true, false>;
-  e.integrate[METHOD][1][1] = launch_integrate<M, METHOD, true, true>;
+  // 'auto' with S <= kHandMaxS integrates through the hand-over queue (integrate_hq / bdf_hq)
+  if constexpr (!kHandQueue<M, METHOD>) {
+    e.integrate[METHOD][0][0] = launch_integrate<M, METHOD, false, false>;
+    e.integrate[METHOD][0][1] = launch_integrate<M, METHOD, false, false>;  // NT only matters with a trajectory
+    e.integrate[METHOD][1][0] = launch_integrate<M, METHOD, true, false>;
+    e.integrate[METHOD][1][1] = launch_integrate<M, METHOD, true, true>;
+  }
   // the stiff methods' MH chains with one lane per chain (S <= kStiffRegS) run as rounds of
   // k_mh_tree + k_mh_resolve, one iteration a round when not speculating (kMhRoundsOnly)
   if constexpr (!kMhRoundsOnly<M, METHOD>) e.mh[METHOD] = launch_mh<M, METHOD>;

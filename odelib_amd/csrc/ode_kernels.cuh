@@ -633,29 +633,40 @@ __device__ __forceinline__ void dp_pipe_publish(DpPipe<S>& pp, double t, double 
   if (pp.lane == 0) *pp.produced = pp.n;
 }
 
-// ---- The hand-over queue of 'auto' (S <= kHandMaxS, small ensembles: k_integrate_hq / k_bdf_hq) ----
+#ifndef OE_LANE_INTEGRATE  // measurement / debug builds: chi-only oe_integrate on the per-lane DOPRI5 too
+#define OE_LANE_INTEGRATE 0
+#endif
+// ---- The hand-over queue of 'auto' (S <= kHandMaxS: k_integrate_hq / k_bdf_hq) ----
 // In k_integrate<M, auto> a lane handed to BDF waits for its wave's whole DOPRI5 pass and then
 // runs its BDF pass in that wave: the wave's time is its DOPRI5 pass plus its slowest handed
-// lane's BDF pass.  The queue splits LSODA's two halves over two kernels that run at the same
-// time on two streams: k_integrate_hq (the lockstep DOPRI5 pass without the BDF code, ~200
-// registers) puts a handed walker's state into a device-memory slot at its eviction point, and
-// k_bdf_hq (one-wave workgroups at ~310 registers: 200 + 312 <= 512, so they sit beside the
-// DOPRI5 waves) takes the slots as they fill, one walker per wave while they fit, and runs the
-// per-lane BDF pass (bdf.cuh).  A per-lane BDF pass does not depend on the lane or wave running
-// it (profiles/NOTES.md r05o): the same bits.  It pays only where the DOPRI5 waves leave SIMDs
-// free — a BDF wave sharing a SIMD with a DOPRI5 wave slows it and is slowed by it — so
-// oe_integrate takes it up to OE_HQ_MAX_W_PER_CU walkers per CU (NOTES round 6: 1 024 walkers
-// with 0.1 % / 1 % stiff 1.94 -> 1.54 / 2.96 -> 1.82 ms; C2's 65 536: 2.56 -> 2.71 / 2.82 ->
-// 6.23, hence in-wave there).  An in-kernel version (BDF waves in the DOPRI5 workgroups) had to
-// fit every wave in 256 registers and its BDF steps ran ~1.5x slower.
-// Protocol (device scope): a producer lane reserves slot j (atomic ctl[0]), writes its state,
+// lane's BDF pass, at the pace of a lane sharing its CU with DOPRI5 waves.  The queue splits
+// LSODA's two halves over two kernels: k_integrate_hq (the lockstep DOPRI5 pass without the
+// BDF code, ~200 registers) puts a handed walker's state into a device-memory slot at its
+// eviction point, and k_bdf_hq (one-wave workgroups, ~310 registers) runs the per-lane BDF
+// pass (bdf.cuh) of each slot, one walker per wave.  Small ensembles (<= OE_HQ_MAX_W_PER_CU
+// walkers per CU) launch k_bdf_hq beside the DOPRI5 kernel on a second stream (200 + 312 <= 512
+// registers per SIMD: the BDF waves sit next to the DOPRI5 waves and start as walkers are
+// handed over); larger ones launch it after the DOPRI5 kernel on the same stream, where every
+// handed walker gets a SIMD of its own instead of one shared with DOPRI5 waves.  A per-lane
+// BDF pass does not depend on the lane or wave running it (profiles/NOTES.md r05o): the same
+// bits as the in-wave pass.  Measured against it (NOTES round 6, r06p; ms, 0.1 % / 1 % stiff):
+// 1 024 walkers 1.92 -> 1.61 / 2.97 -> 1.79; 4 096: 2.09 -> 1.79 / 3.17 -> 1.80; 16 384: 2.35 ->
+// 2.19 / 3.09 -> 2.22; 65 536 (C2): 2.49 -> 2.37 / 2.85 -> 2.87; none stiff: within 0.05 ms.
+// Rejected on the way: BDF waves inside the DOPRI5 workgroups (every wave then gets 256
+// registers; BDF steps ~1.5x slower), the BDF kernel beside the DOPRI5 kernel for large
+// ensembles (each BDF wave shares a SIMD with an issue-bound DOPRI5 wave: C2 + 1 % stiff
+// 6.2 ms), slots claimed by CAS (a thousand waves on one counter: claims over 6.7 ms).
+// Protocol (device scope): a producer lane reserves slot j (atomic ctl[0]), writes its state
 // and publishes ready[j] = epoch with a release store; each producer wave adds one to ctl[2]
-// after its pass.  A BDF wave claims a run of reserved slots (CAS on ctl[1]), waits for their
-// ready flags and leaves once every producer wave is counted and no reserved slot is unclaimed.
-// Producers never wait on the BDF kernel, so any schedule of the two kernels finishes (run one
-// after the other, the queue is simply full when BDF starts); a BDF wave also leaves, flagging
-// ctl[3], past kHandTimeout.
+// after its pass.  BDF wave g's lane l takes slot g + l·G and waits until it is published or
+// every producer wave is done without having reserved it.  Producers never wait on the BDF
+// kernel, so any schedule of the two kernels finishes; a BDF wave also leaves, flagging ctl[3],
+// past kHandTimeout.
 constexpr int kHandMaxS = 4;  // the co-residency budget above (S = 5..8 keep the in-wave pass)
+// the built-in models whose 'auto' integrate runs through the queue (always: OE_LANE_INTEGRATE
+// measurement builds keep k_integrate's per-lane path instead)
+template <class M, int METHOD>
+constexpr bool kHandQueue = METHOD == kAuto && M::S <= kHandMaxS && !OE_LANE_INTEGRATE;
 #ifndef OE_HQ_MAX_W_PER_CU  // oe_integrate takes the queue up to this many walkers per CU (r06i:
 #define OE_HQ_MAX_W_PER_CU 16  // W = 1 024 / 4 096 win 20-40 %, 16 384 mixed, 65 536 loses)
 #endif
@@ -665,8 +676,8 @@ constexpr int kHandMaxS = 4;  // the co-residency budget above (S = 5..8 keep th
 #ifndef OE_HQ_MIX  // measurement builds: 0 = every tableau coefficient in VGPRs (breaks the budget)
 #define OE_HQ_MIX 1
 #endif
-#ifndef OE_HQ_WAVES  // measurement builds: one-wave workgroups of k_bdf_hq (capped at 4 per CU)
-#define OE_HQ_WAVES 1024
+#ifndef OE_HQ_WAVES  // measurement builds: the most one-wave workgroups of k_bdf_hq
+#define OE_HQ_WAVES 4096
 #endif
 #ifndef OE_HQ_PRIO  // measurement builds: 0 = the BDF waves at the default priority
 #define OE_HQ_PRIO 1
@@ -678,7 +689,8 @@ constexpr uint64_t kHandTimeout = 6000000000ull;  // s_memrealtime ticks (100 MH
 struct HandQ {
   double* d;        // [(S + 5)][cap]: y[0..S), t, chi, ssres, nf, ymin
   int32_t* n;       // [6][cap]: i, k, nvalid, status, walker, ready
-  int32_t* ctl;     // [0] reserved, [1] claimed, [2] producer waves done, [3] timeout
+  int32_t* ctl;     // [0] reserved, [1] claimed, [2] producer waves done, [3] timeout, [4] BDF waves
+                    // that claimed or left (trace builds: [6..9] two 64-bit clocks)
   int32_t cap;      // slots (>= walkers of the launch)
   int32_t epoch;    // ready[j] == epoch: slot j of this launch is published
   int32_t n_waves;  // producer waves of the launch
@@ -1101,9 +1113,6 @@ namespace oe {
 // walker (stiff_wave.cuh).  The MH kernel redoes them in place (private-memory path).
 // LANE (kernels without a trajectory, S <= 8): DOPRI5 with a step size per lane (lane.cuh)
 // instead of one per wave.
-#ifndef OE_LANE_INTEGRATE  // measurement / debug builds: chi-only oe_integrate on the per-lane DOPRI5 too
-#define OE_LANE_INTEGRATE 0
-#endif
 template <class M, int METHOD>
 constexpr bool kLaneSteps = (METHOD == kDOPRI5 || METHOD == kAuto || METHOD == kBdf) && M::S <= kStiffRegS;
 
@@ -1275,7 +1284,7 @@ __global__ void __launch_bounds__(256) k_integrate_hq(const DevProblem pb, const
   static_assert(S <= kHandMaxS, "the hand-over queue's co-residency budget");
 #if OE_HQ_TRACE
   if (blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_store((uint64_t*)(hq.ctl + 4), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+    __hip_atomic_store((uint64_t*)(hq.ctl + 6), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 #endif
   const int64_t blk = ia.xcd_remap ? xcd_block(blockIdx.x, gridDim.x, ia.xcd_remap) : (int64_t)blockIdx.x;
@@ -1298,7 +1307,7 @@ __global__ void __launch_bounds__(256) k_integrate_hq(const DevProblem pb, const
   }
 #if OE_HQ_TRACE
   if ((threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_max((uint64_t*)(hq.ctl + 6), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+    __hip_atomic_fetch_max((uint64_t*)(hq.ctl + 8), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 #endif
   // this wave's pass is over (its slots were published, each with its own release store; the
@@ -1307,7 +1316,14 @@ __global__ void __launch_bounds__(256) k_integrate_hq(const DevProblem pb, const
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(hq.ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr int kHandBdfWaves = OE_HQ_WAVES;  // k_bdf_hq workgroups (one wave each): 4 per CU, one per SIMD
+constexpr int kHandBdfWaves = OE_HQ_WAVES;  // k_bdf_hq workgroups at most (one wave each)
+// Slots are dealt statically: BDF wave g's lane l takes slot g + l·G (G = the kernel's waves),
+// so each handed walker is alone in its wave while there are no more than G of them, and no
+// wave claims anything (a CAS claim by a thousand waves on one counter serialised the claims:
+// 655 walkers were picked up over 6.7 ms, r06n).  A lane waits until its slot is published or
+// every producer wave is done without reaching it; no loop runs around the BDF pass, so the
+// pass's loop-invariant constants are formed after the wait instead of in the prologue, where
+// they lived across the polling in SGPRs spilled to VGPR lanes (111 spilled SGPRs -> 21).
 template <class M, bool TRAJ, bool NT>
 __global__ void __launch_bounds__(64) k_bdf_hq(const DevProblem pb, const IntegrateArgs ia, const HandQ hq) {
   constexpr int S = M::S;
@@ -1315,97 +1331,66 @@ __global__ void __launch_bounds__(64) k_bdf_hq(const DevProblem pb, const Integr
   const int lane = (int)threadIdx.x;
   const int64_t W = ia.W, c = hq.cap;
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  const int64_t slot = (int64_t)blockIdx.x + (int64_t)lane * gridDim.x;
+  bool part = slot < W;
   for (;;) {
-    // lane 0 claims a run of reserved slots
-    int base = -1, m = 0;
-    if (lane == 0) {
-      for (;;) {
-        const int done = hq_load(hq.ctl + 2);
-        const int r = hq_load(hq.ctl);
-        int cl = hq_load(hq.ctl + 1);
-        if (r > cl) {
-          // one walker per BDF wave while the pending ones fit the kernel's waves: a lone lane
-          // runs the pass fastest (a wave's batch waits for its slowest walker); beyond that,
-          // the backlog shared out
-          const int want = min(64, max(1, (r - cl) / (int)gridDim.x));
-          if (__hip_atomic_compare_exchange_strong(hq.ctl + 1, &cl, cl + want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)) {
-            base = cl;
-            m = want;
-            break;
-          }
-          continue;
-        }
-        if (done >= hq.n_waves) {  // every producer wave counted: `reserved` is final
-          hq_acquire();
-          if (hq_load(hq.ctl) <= hq_load(hq.ctl + 1)) break;
-          continue;
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t_start > kHandTimeout) {
-          __hip_atomic_store(hq.ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        // ~OE_HQ_POLL x 8 000 cycles between polls: a few hundred pollers must not load the
-        // queue's control line (or the memory side behind it) the DOPRI5 kernel also uses
-        for (int z = 0; z < OE_HQ_POLL; ++z) __builtin_amdgcn_s_sleep(127);
+    bool wait = false;
+    if (part && hq_load(hq.n + 5 * c + slot) != hq.epoch) {
+      // not (yet) published: a producer will, unless every producer wave is done without
+      // having reserved this slot
+      if (hq_load(hq.ctl + 2) >= hq.n_waves) {
+        hq_acquire();
+        if (hq_load(hq.ctl) <= slot) part = false;
+        else wait = true;  // reserved: its data is on the way
+      } else {
+        wait = true;
       }
     }
-    base = __shfl(base, 0);
-    m = __shfl(m, 0);
-    if (base < 0) break;
-    const bool part = lane < m;
-    const int j = base + (part ? lane : 0);
-    // a claimed slot is reserved: its producer lane is writing it
-    bool late = false;
-    for (;;) {
-      const bool ok = !part || hq_load(hq.n + 5 * c + j) == hq.epoch;
-      if (__ballot(!ok) == 0ull) break;
-      if (__builtin_amdgcn_s_memrealtime() - t_start > kHandTimeout) {
-        late = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (late) {
+    if (__ballot(wait) == 0ull) break;
+    if (__builtin_amdgcn_s_memrealtime() - t_start > kHandTimeout) {
       if (lane == 0) __hip_atomic_store(hq.ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
+      return;
     }
-    hq_acquire();  // the slots' data, published by their producers' release stores
-    double y[S], p[PMAX];
+    // ~OE_HQ_POLL x 8 000 cycles between polls: a few thousand pollers must not load the
+    // queue's lines (or the memory side behind them) the DOPRI5 kernel also uses
+    for (int z = 0; z < OE_HQ_POLL; ++z) __builtin_amdgcn_s_sleep(127);
+  }
+  if (__ballot(part) == 0ull) return;
+  const int64_t j = part ? slot : 0;
+  hq_acquire();  // the slots' data, published by their producers' release stores
+  double y[S], p[PMAX];
 #pragma unroll
-    for (int s = 0; s < S; ++s) y[s] = hq.d[s * c + j];
-    const double t = hq.d[S * c + j];
-    Acc a{hq.d[(S + 1) * c + j], hq.d[(S + 2) * c + j], hq.d[(S + 3) * c + j], hq.d[(S + 4) * c + j],
-          hq.n[2 * c + j], hq.n[3 * c + j]};
-    const int i = hq.n[j], k = hq.n[c + j];
-    const int64_t w = hq.n[4 * c + j];
+  for (int s = 0; s < S; ++s) y[s] = hq.d[s * c + j];
+  const double t = hq.d[S * c + j];
+  Acc a{hq.d[(S + 1) * c + j], hq.d[(S + 2) * c + j], hq.d[(S + 3) * c + j], hq.d[(S + 4) * c + j],
+        hq.n[2 * c + j], hq.n[3 * c + j]};
+  const int i = hq.n[j], k = hq.n[c + j];
+  const int64_t w = hq.n[4 * c + j];
 #pragma unroll
-    for (int q = 0; q < PMAX; ++q) p[q] = (q < pb.P) ? ia.theta[(int64_t)q * W + w] : 0.0;
+  for (int q = 0; q < PMAX; ++q) p[q] = (q < pb.P) ? ia.theta[(int64_t)q * W + w] : 0.0;
 #if OE_HQ_TRACE
-    const uint64_t t_claim = __builtin_amdgcn_s_memrealtime();
+  const uint64_t t_claim = __builtin_amdgcn_s_memrealtime();
 #endif
-    // The BDF pass is one lane's dependency chain (latency-bound, sparse issue); the DOPRI5
-    // wave sharing its SIMD is issue-bound.  At a higher priority the BDF wave issues whenever
-    // it is ready, taking few slots from the DOPRI5 wave, instead of waiting behind it.
-    if (OE_HQ_PRIO) __builtin_amdgcn_s_setprio(3);
-    integrate_bdf_lane<M, PMAX, TRAJ, NT, 64>(pb, y, t, i, k, p, ia.traj, W, w, part, part, a);
-    if (OE_HQ_PRIO) __builtin_amdgcn_s_setprio(0);
+  // The BDF pass is one lane's dependency chain (latency-bound, sparse issue); the DOPRI5
+  // wave sharing its SIMD is issue-bound.  At a higher priority the BDF wave issues whenever
+  // it is ready, taking few slots from the DOPRI5 wave, instead of waiting behind it.
+  if (OE_HQ_PRIO) __builtin_amdgcn_s_setprio(3);
+  integrate_bdf_lane<M, PMAX, TRAJ, NT, 64>(pb, y, t, i, k, p, ia.traj, W, w, part, part, a);
 #if OE_HQ_TRACE
-    {
-      const uint64_t t0 = __hip_atomic_load((const uint64_t*)(hq.ctl + 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // s_memrealtime: 100 MHz; chi = start·1e5 + the DOPRI5 kernel's last wave end, ssres =
-      // claim·1e5 + BDF pass, all in whole µs from the DOPRI5 kernel's first wave
-      const uint64_t t_pend = __hip_atomic_load((const uint64_t*)(hq.ctl + 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a.chi = (double)((int64_t)(t_start - t0) / 100) * 1e5 + (double)((int64_t)(t_pend - t0) / 100);
-      a.ssres = (double)((int64_t)(t_claim - t0) / 100) * 1e5 + (double)((__builtin_amdgcn_s_memrealtime() - t_claim) / 100);
-      a.nvalid = 1;
-    }
+  {
+    // s_memrealtime: 100 MHz; chi = start·1e5 + the DOPRI5 kernel's last wave end, ssres =
+    // claim·1e5 + BDF pass, all in whole µs from the DOPRI5 kernel's first wave
+    const uint64_t t0 = __hip_atomic_load((const uint64_t*)(hq.ctl + 4 + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t_pend = __hip_atomic_load((const uint64_t*)(hq.ctl + 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.chi = (double)((int64_t)(t_start - t0) / 100) * 1e5 + (double)((int64_t)(t_pend - t0) / 100);
+    a.ssres = (double)((int64_t)(t_claim - t0) / 100) * 1e5 + (double)((__builtin_amdgcn_s_memrealtime() - t_claim) / 100);
+    a.nvalid = 1;
+  }
 #endif
-    if (part) {
-      if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
-      if (ia.ssres) ia.ssres[w] = a.ssres;
-      if (ia.status) ia.status[w] = finish(a);
-    }
+  if (part) {
+    if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");
+    if (ia.ssres) ia.ssres[w] = a.ssres;
+    if (ia.status) ia.status[w] = finish(a);
   }
 }
 

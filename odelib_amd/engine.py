@@ -247,7 +247,7 @@ class Engine:
     # -- batched integrate -------------------------------------------------------------------
     def integrate(self, y0, theta, trajectory: bool = True, traj_out=None, nt_stores: bool = True,
                   sync: bool = True, pipelined=None, half_waves: bool = False,
-                  xcd_remap=True, timing: bool = True, split: bool = True, kernel=None, handq: bool = True):
+                  xcd_remap=True, timing: bool = True, split: bool = True, kernel=None):
         """y0 [S][W], theta [P][W] → dict(traj [T][S][W] | None, chi [W], ssres [W], status [W]).
 
         ``pipelined=True`` (or 2, 4, 8: store waves per 4 compute waves) selects the
@@ -263,10 +263,7 @@ class Engine:
         rule: 32 walkers per wave for 5+ states at <= 1 wave per SIMD), "half", "pipe2",
         "pipe4", "pipe8" (blockIdx order), "pipe2x", "pipe4x", "pipe8x" (XCD runs), or "auto" (OE_TUNE: the library measures the available ones for
         this shape on the first call and keeps the fastest; ``last_variant()`` says which
-        ran).  All of them produce the same bits.
-        ``handq=False`` (method 'auto', built-in models up to 4 states) runs each handed
-        walker's BDF pass in its DOPRI5 wave after that wave's DOPRI5 pass, instead of in the
-        BDF kernel that runs beside the DOPRI5 kernel (OE_NO_HANDQ; same bits)."""
+        ran).  All of them produce the same bits."""
         torch = self.torch
         if kernel is not None:
             if kernel not in ("auto",) + N.KERNEL_NAMES[:-1]:
@@ -295,8 +292,7 @@ class Engine:
             | (N.OE_XCD_RANGES if xcd_remap == "ranges" else 0 if xcd_remap else N.OE_NO_XCD_REMAP) \
             | (0 if timing else N.OE_NO_TIMING) | (0 if split else N.OE_NO_SPLIT) \
             | (N.OE_TUNE if kernel == "auto" else 0) \
-            | (N.OE_PIPE_XCD if kernel is not None and kernel.endswith("x") else 0) \
-            | (0 if handq else N.OE_NO_HANDQ)
+            | (N.OE_PIPE_XCD if kernel is not None and kernel.endswith("x") else 0)
         self.ctx.integrate(W, _ptr(y0), _ptr(theta), _ptr(traj), _ptr(chi), _ptr(ssres), _ptr(status), flags)
         if sync:
             torch.cuda.synchronize(self.dev)

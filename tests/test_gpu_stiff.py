@@ -89,19 +89,18 @@ def test_auto_moderately_stiff_walkers_bitwise_vs_c_restatement():
     assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == [5, 40, 64, 100, 129]
 
 
-@pytest.mark.parametrize("trajectory", [True, False])
-def test_auto_hand_over_queue_many_walkers_bitwise(trajectory):
+@pytest.mark.parametrize("W,trajectory", [(600, True), (600, False), (8192, True)])
+def test_auto_hand_over_queue_many_walkers_bitwise(W, trajectory):
     """'auto' hands stiff walkers through the hand-over queue (ode_kernels.cuh HandQ: the DOPRI5
     kernel publishes each at its eviction point, the BDF kernel beside it takes them): many
-    handed walkers in one workgroup (150 of block 1's 256, more than one BDF wave's batch),
+    handed walkers in one workgroup (150 of block 1's 256),
     handed at different times (tau from 1e3 to 1e5), one in the partial last block, blocks
-    without any — the same bits as the C restatement and as the in-wave pass (OE_NO_HANDQ),
-    whatever wave ran a walker's BDF pass."""
+    without any — the same bits as the C restatement, whatever wave ran a walker's BDF pass;
+    at 600 walkers the BDF kernel runs beside the DOPRI5 kernel, at 8 192 after it."""
     m = product_model("two_i", method="auto")
-    W = 600  # (<= 16 walkers per CU: the queue's range)
     theta = walker_thetas("two_i", W, seed=5).T.copy()
     rs = np.random.RandomState(11)
-    lanes = sorted(set(rs.choice(np.arange(256, 512), 150, replace=False).tolist()) | {3, 599})
+    lanes = sorted(set(rs.choice(np.arange(256, 512), 150, replace=False).tolist()) | {3, W - 1})
     taus = (1e3, 3e3, 1e4, 1e5)
     for j, w in enumerate(lanes):
         theta[4, w] = taus[j % len(taus)]
@@ -113,10 +112,6 @@ def test_auto_hand_over_queue_many_walkers_bitwise(trajectory):
     np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
     np.testing.assert_allclose(out["ssres"], ref["ssres"], rtol=1e-12)
     assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == lanes
-    inwave = m.engine().integrate(y0, theta, trajectory=trajectory, handq=False)
-    for k in ("traj", "chi", "ssres", "status"):
-        if out[k] is not None:
-            assert np.array_equal(out[k], inwave[k].cpu().numpy(), equal_nan=True), k
 
 
 @pytest.mark.parametrize("method", ["rosenbrock", "bdf"])

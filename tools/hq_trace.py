@@ -36,6 +36,7 @@ def main():
     dur = ss - claim * 1e5
     order = np.argsort(claim + dur)
     print(json.dumps({"kernel_ms": ms, "n": int(n), "dopri5_end_us": float(np.max(pend)),
+                      "claim_spread_us": float(np.max(claim) - np.min(claim)),
                       "wave_start_us": [float(np.min(chi)), float(np.median(chi)), float(np.max(chi))],
                       "claim_us": [float(np.min(claim)), float(np.median(claim)), float(np.max(claim))],
                       "bdf_us": [float(np.min(dur)), float(np.median(dur)), float(np.max(dur))],

@@ -28,7 +28,6 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--trajectory", type=int, default=1)
     ap.add_argument("--contiguous", action="store_true", help="the stiff walkers are walkers 0..n-1 (one wave's lanes)")
-    ap.add_argument("--handq", type=int, default=1, help="0: 'auto' with the in-wave BDF pass (OE_NO_HANDQ)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -56,15 +55,14 @@ def main():
                 eng = engines[method]
                 ms = []
                 for r in range(args.reps + 1):
-                    kw = {} if args.handq else {"handq": False}
-                    out = eng.integrate(y0, theta, trajectory=bool(args.trajectory), traj_out=traj, sync=True, **kw)
+                    out = eng.integrate(y0, theta, trajectory=bool(args.trajectory), traj_out=traj, sync=True)
                     if r:
                         ms.append(eng.last_kernel_ms())
                 st = out["status"].cpu().numpy()
                 print(json.dumps({"model": args.model, "walkers": W, "stiff_frac": frac, "tau": tau, "method": method,
                                   "kernel_ms": round(float(np.median(ms)), 4),
                                   "stiff_flagged": int(((st & 8) != 0).sum()), "maxstep": int(((st & 4) != 0).sum()),
-                                  "trajectory": bool(args.trajectory), "handq": args.handq}), flush=True)
+                                  "trajectory": bool(args.trajectory)}), flush=True)
 
 
 if __name__ == "__main__":
