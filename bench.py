@@ -89,6 +89,9 @@ def parse():
                     help="wide chain models' DOPRI5: one lane per walker instead of the split kernel")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg (1 048 576 walkers over the ranks)")
     ap.add_argument("--c4-steps", type=int, default=10, help="C4 leg: timed trajectory integrates")
+    ap.add_argument("--comm-timeout", type=float, default=180.0,
+                    help="C4 leg: a rank whose communicator set-up, all-gather or barrier has not returned "
+                         "after this many seconds names the call on stderr and exits 87 (no hang)")
     ap.add_argument("--pool", default="cabi", choices=["cabi", "torch"],
                     help="C4 posterior pooling: the C-ABI's RCCL communicator (oe_allgather_samples, what "
                          "ODElib binds) or torch.distributed's all_gather_into_tensor")
@@ -516,17 +519,23 @@ class Ranks:
         self.dev_index = local_rank % max(ndev, 1)
         torch.cuda.set_device(self.dev_index)
         self.dev = torch.device("cuda", self.dev_index)
+        self.comm_timeout = float(os.environ.get("ODELIB_BENCH_COMM_TIMEOUT", "180"))
         if world > 1:
-            if self.backend == "nccl":
-                dist.init_process_group("nccl", device_id=self.dev)
-            else:
-                dist.init_process_group(self.backend)
+            from odelib_amd.distributed import watch
+            with watch(f"init_process_group ({self.backend})", rank, self.comm_timeout):
+                if self.backend == "nccl":
+                    dist.init_process_group("nccl", device_id=self.dev)
+                else:
+                    dist.init_process_group(self.backend)
         self.red_dev = self.dev if self.backend == "nccl" else torch.device("cpu")
 
     def fence(self):
-        """barrier + synchronize (both sides of every timed region)."""
+        """barrier + synchronize (both sides of every timed region); a barrier that has not
+        returned after the communication timeout names itself and ends the rank (exit 87)."""
         if self.world > 1:
-            self.dist.barrier()
+            from odelib_amd.distributed import watch
+            with watch("barrier", self.rank, self.comm_timeout, log=False):
+                self.dist.barrier()
         self.torch.cuda.synchronize(self.dev)
 
     def max(self, *vals):
@@ -673,49 +682,70 @@ def c4_leg(args, R, T, P):
     res["posterior_block_bytes_per_rank"] = blk.numel() * 8
     pool = args.pool if (R.world == 1 or R.backend == "nccl") else "torch"
     cabi_error = None
+    from odelib_amd.distributed import watch
+
+    def w(what):  # every collective of the pooling, named in the log and bounded (no hang)
+        return watch(f"C4 {what}", R.rank, args.comm_timeout, log=R.world > 1)
     if pool == "cabi":
-        # Every rank takes the same path: the communicator set-up and the untimed first
-        # gather are agreed on by an all-reduce of an error flag before the timed gather,
-        # and its outcome after it — a rank that fell back alone would enter a different
-        # collective than its peers and the job would hang.
+        # Every rank takes the same path: an error RAISED by the communicator set-up or the
+        # untimed first gather is agreed on by an all-reduce of an error flag before the timed
+        # gather, and the timed gather's outcome after it — a rank that fell back alone would
+        # enter a different collective than its peers.  A rank that never returns from one of
+        # these calls is named and ended by watch() (a peer already inside the collective
+        # cannot be released by a flag).
         from odelib_amd.distributed import native_allgather_walkers, native_comm
         comm, pooled = None, None
         try:
             try:
-                comm = native_comm(R.dev.index, None)
+                with w("oe_comm_init (rank 0's id broadcast, ncclCommInitRank)"):
+                    comm = native_comm(R.dev.index, None)
                 src = blk.contiguous()
-                native_allgather_walkers(src[:1], C4_WALKERS if R.world > 1 else cnt, comm)  # untimed: channel set-up
+                with w("oe_allgather_samples, untimed first"):
+                    native_allgather_walkers(src[:1], C4_WALKERS if R.world > 1 else cnt, comm)
+                    torch.cuda.synchronize(R.dev)
                 ok = 1.0
             except Exception as e:  # an error raised by the C-ABI path (not a hang)
                 cabi_error, ok = f"{type(e).__name__}: {e}"[:300], 0.0
-            if -R.max(-ok) > 0.0:  # min over ranks: every rank set up its communicator
-                R.fence()
+            with w("error-flag all-reduce"):
+                agreed = -R.max(-ok) > 0.0  # min over ranks: every rank set up its communicator
+            if agreed:
+                with w("barrier before the timed gather"):
+                    R.fence()
                 t0 = time.perf_counter()
                 try:
-                    pooled = native_allgather_walkers(src, C4_WALKERS if R.world > 1 else cnt, comm)
+                    with w("oe_allgather_samples, timed"):
+                        pooled = native_allgather_walkers(src, C4_WALKERS if R.world > 1 else cnt, comm)
+                        torch.cuda.synchronize(R.dev)
                     ok = 1.0
                 except Exception as e:
                     cabi_error, ok, pooled = f"{type(e).__name__}: {e}"[:300], 0.0, None
-                R.fence()
+                with w("barrier after the timed gather"):
+                    R.fence()
                 t_ag = R.max(time.perf_counter() - t0)
                 n_ranks = comm.n_ranks
-                if -R.max(-ok) == 0.0:
-                    pooled = None
+                with w("error-flag all-reduce after the gather"):
+                    if -R.max(-ok) == 0.0:
+                        pooled = None
             if pooled is None:  # some rank failed: all pool with torch, and say so
                 cabi_error = cabi_error or "another rank's C-ABI pooling failed"
                 pool = "torch"
         finally:
             if comm is not None:
-                comm.close()
+                with w("oe_comm_destroy"):
+                    comm.close()
     if pool == "cabi":
         pass
     elif R.world > 1:
         src = blk.contiguous() if R.backend == "nccl" else blk.cpu()
-        allgather_walkers(src[:1], C4_WALKERS)  # untimed: communicator / channel set-up
-        R.fence()
+        with w("torch all_gather, untimed first"):
+            allgather_walkers(src[:1], C4_WALKERS)  # communicator / channel set-up
+        with w("barrier before the timed gather"):
+            R.fence()
         t0 = time.perf_counter()
-        pooled = allgather_walkers(src, C4_WALKERS)
-        R.fence()
+        with w("torch all_gather, timed"):
+            pooled = allgather_walkers(src, C4_WALKERS)
+        with w("barrier after the timed gather"):
+            R.fence()
         t_ag = R.max(time.perf_counter() - t0)
         n_ranks = R.world
     else:
@@ -925,6 +955,7 @@ def main():
     import numpy as np
     import torch
 
+    os.environ.setdefault("ODELIB_BENCH_COMM_TIMEOUT", str(args.comm_timeout))
     R = Ranks(world, rank, local_rank)
     eng, _ = R.engine(args.model, args.method, args.times)
     dev = R.dev

@@ -121,7 +121,7 @@ def batched_metropolis_hastings(chains, nits=1000, burnin=None, static_parameter
              are bitwise the same either way, for every method: the MH kernels integrate
              every proposal on its own (DOPRI5 step sizes per chain, csrc/lane.cuh; the BDF
              hand-over of 'auto' and method 'bdf' with step sizes and orders per chain,
-             csrc/bdf_lane.cuh), so a chain does not depend on the chains that share its
+             csrc/bdf.cuh integrate_bdf_lane), so a chain does not depend on the chains that share its
              wavefront, the speculation depth or the device's CU count."""
     m0 = chains[0]
     pnames = m0.get_pnames()

@@ -142,9 +142,13 @@ struct SplitOf { static constexpr int K = 0; };
 template <int N>
 struct SplitOf<Chain<N>> { static constexpr int K = split_lanes_chain<N>(); };
 #ifdef OE_SPLIT_TWOI  // measurement builds: two_i (Chain<4>'s RHS, operation for operation) over 2 or 4 lanes
+static_assert(OE_SPLIT_TWOI == 2 || OE_SPLIT_TWOI == 4, "OE_SPLIT_TWOI: 2 or 4 lanes per walker (=2 or =4, not bare)");
 template <>
 struct SplitOf<TwoI> { static constexpr int K = OE_SPLIT_TWOI; };
 #endif
+// The split kernels are DOPRI5's only (mh_split / dopri5_split): no 'auto' / 'bdf' launch takes
+// them, so the per-lane BDF pass and its deferred-observation scratch (DevProblem::obs_c,
+// which oe_mh_run leaves null for split launches) never meet a split walker.
 
 template <class M, int METHOD>
 void fill_method(Entry& e) {

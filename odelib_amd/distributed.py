@@ -10,7 +10,48 @@ pooled by ONE all-gather (RCCL over xGMI with the ``nccl`` backend; gloo on CPU)
 """
 from __future__ import annotations
 
+import contextlib
+import os
+import sys
+import threading
+import time
+
 import numpy as np
+
+
+@contextlib.contextmanager
+def watch(what: str, rank: int, timeout_s: float = 180.0, log: bool = True):
+    """Name a collective (or a communicator set-up) in this rank's log and bound it.
+
+    Entry and exit go to stderr as ``[rank r +t s] what: enter / exit (dt s)``, so a multi-
+    rank run that stalls shows from its tail alone which rank is inside which call.  If the
+    call has not returned after ``timeout_s`` the rank prints ``... did not return`` and ends
+    the process with exit status 87 instead of hanging (os._exit from a watchdog thread: the
+    collective cannot be interrupted; the launcher then tears the job down).  The multi-GPU
+    pooling path of the reference is ``Pool.starmap`` + ``pd.concat`` (Framework.py:779-780,
+    :1037); its RCCL analogue first runs with more than one rank on an 8-GPU node."""
+    t0 = time.perf_counter()
+    stamp = lambda: f"[rank {rank} +{time.perf_counter() - _T0:.3f} s]"  # noqa: E731
+    if log:
+        print(f"{stamp()} {what}: enter", file=sys.stderr, flush=True)
+
+    def expire():
+        print(f"{stamp()} {what}: did not return within {timeout_s:.0f} s — exiting (87)", file=sys.stderr,
+              flush=True)
+        os._exit(87)
+
+    timer = threading.Timer(timeout_s, expire)
+    timer.daemon = True
+    timer.start()
+    try:
+        yield
+    finally:
+        timer.cancel()
+        if log:
+            print(f"{stamp()} {what}: exit ({time.perf_counter() - t0:.3f} s)", file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
 
 
 def shard(n_total: int, rank: int, world: int) -> tuple[int, int]:
@@ -92,7 +133,7 @@ def sharded_mh(engine, theta_all, y0_all, nits: int, burnin: int, walk_mask, ini
     small to fill their device).  The draws are keyed by global walker id and iteration, and
     in the MH kernels every chain is integrated on its own — DOPRI5 step sizes per chain
     (csrc/lane.cuh) and, for 'auto' / 'bdf', BDF step sizes and orders per chain
-    (csrc/bdf_lane.cuh) — so with RK4, DOPRI5, 'auto' and 'bdf' the pooled chains are bitwise
+    (csrc/bdf.cuh integrate_bdf_lane) — so with RK4, DOPRI5, 'auto' and 'bdf' the pooled chains are bitwise
     those of one sequential launch for any rank count and speculation depth (models of up to
     8 states; the split wide-chain kernels group 64/K chains per step size), as the
     reference's chains, one odeint call per proposal (Framework.py:656, :779-780), never

@@ -1290,7 +1290,7 @@ static void auto_group(const Prob* pb, Lane* L, int nl, const double* p, double*
       any |= L[l].part;
       if (L[l].part) L[l].a.status |= ST_STIFF;
     }
-    /* every handed lane on its own: the device's BDF pass (bdf_lane.cuh) gives each lane
+    /* every handed lane on its own: the device's BDF pass (bdf.cuh integrate_bdf_lane) gives each lane
        its own step size and order, in every kernel */
     if (any)
       for (int l = 0; l < nl; ++l)

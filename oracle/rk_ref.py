@@ -101,7 +101,7 @@ def product_split(fp) -> int:
 
 def lane_steps(fp) -> bool:
     """Whether the product's MH kernels step every chain on its own (ode_kernels.cuh
-    kLaneSteps, lane.cuh, bdf_lane.cuh): DOPRI5 / 'auto' / 'bdf', one lane per walker, at most
+    kLaneSteps, lane.cuh, bdf.cuh integrate_bdf_lane): DOPRI5 / 'auto' / 'bdf', one lane per walker, at most
     8 states — step sizes (and BDF orders) per walker, not per lockstep group."""
     return fp.method in ("dopri5", "auto", "bdf") and int(fp.n_states) <= 8 and product_split(fp) == 1
 

@@ -99,3 +99,23 @@ def test_gloo_world2_sharded_mh_matches_single_process():
     for j in range(5):  # Framework.py:11-17 on the concatenated posterior column
         m_ref, s_ref = rawstats(pd.Series(pooled[:, j, :].reshape(-1)))
         np.testing.assert_allclose([med[j], sd[j]], [m_ref, s_ref], rtol=1e-12)
+
+
+def test_collective_watch_names_a_stalled_call_and_exits():
+    """bench.py's C4 pooling and barriers run inside distributed.watch: a call that does not
+    return within its bound is named on stderr with the rank, and the rank exits 87 instead of
+    hanging (a failing first 8-rank RCCL run must be diagnosable from the
+    driver's tail alone)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, time; sys.path.insert(0, %r)\n"
+            "from odelib_amd.distributed import watch\n"
+            "with watch('C4 oe_allgather_samples, timed', 3, 0.5):\n"
+            "    pass\n"
+            "with watch('C4 barrier after the timed gather', 3, 0.5):\n"
+            "    time.sleep(30)\n") % root
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 87, (r.returncode, r.stderr)
+    assert "[rank 3" in r.stderr and "C4 oe_allgather_samples, timed: exit" in r.stderr, r.stderr
+    assert "C4 barrier after the timed gather: did not return within" in r.stderr, r.stderr

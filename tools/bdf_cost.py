@@ -1,5 +1,5 @@
 """What one BDF step costs on the device: the trajectory kernels' lockstep pass (bdf.cuh,
-chi-only integrate) against the MH kernels' per-lane pass (bdf_lane.cuh, the a-priori fit
+chi-only integrate) against the MH kernels' per-lane pass (bdf.cuh integrate_bdf_lane, the a-priori fit
 of an mh_run with nits = 1), method 'bdf' (BDF from t0, no DOPRI5 phase), per step of the
 slowest lane (C restatement's counts: accepted + rejected attempts).
 
