@@ -799,7 +799,7 @@ int oe_problem_set(oe_ctx* c, const oe_problem* p) {
       }
       if (cm->rtc.stiff != 1) return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: " + cm->rtc.stiff_err);
     } else if (e->integrate[p->method][0][0] == nullptr &&
-               !(p->method == OE_METHOD_AUTO && e->integrate_hq[0][0] != nullptr)) {
+               !(p->method == OE_METHOD_AUTO && e->integrate_hq[0][0][0] != nullptr)) {
       return fail(c, OE_ERR_UNSUPPORTED, "oe_problem_set: the stiff methods (auto, rosenbrock) need n_states <= " +
                                              std::to_string(kStiffMaxS));
     }
@@ -1015,7 +1015,7 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
     // second stream for small ensembles (<= OE_HQ_MAX_W_PER_CU walkers per CU), else after it
     // on the same stream; the caller's stream waits for both
     const int tj = ia.traj ? 1 : 0, nj = nt ? 1 : 0;
-    const bool handq = c->method == OE_METHOD_AUTO && !e->rtc && e->integrate_hq[tj][nj] && !OE_LANE_INTEGRATE;
+    const bool handq = c->method == OE_METHOD_AUTO && !e->rtc && e->integrate_hq[0][tj][nj] && !OE_LANE_INTEGRATE;
     const bool beside = W <= (int64_t)OE_HQ_MAX_W_PER_CU * c->n_cu;  // else: after the DOPRI5 kernel
     if (handq) {
       HandQ q{};
@@ -1029,7 +1029,7 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
         OE_HIP(c, hipStreamWaitEvent(c->hq_stream, c->ev_hq[0], 0));
         bs = c->hq_stream;
       }
-      e->integrate_hq[tj][nj](c->dp, ia, q, grid, block, c->stream);
+      e->integrate_hq[beside ? 1 : 0][tj][nj](c->dp, ia, q, grid, block, c->stream);
       OE_HIP(c, hipGetLastError());
       // one wave per walker (slots dealt statically, k_bdf_hq): beside the DOPRI5 kernel up to
       // kHandBdfWaves, after it one wave per SIMD (a round of dispatch when nothing was handed)

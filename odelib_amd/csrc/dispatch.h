@@ -29,9 +29,10 @@ struct Entry {
   IntegrateLaunch integrate[kMethods][2][2];
   IntegrateLaunch rk4_piped[3][2];  // [2, 4, 8 store waves][nt]; null when S > OE_PIPE_MAX_S
   IntegrateLaunch dopri5_piped[2];  // [nt]: DOPRI5 trajectories through store waves; null when S > 6
-  // 'auto' through the hand-over queue, [traj][nt] (S <= kHandMaxS): the DOPRI5 kernel and the
-  // BDF kernel beside it
-  HandQLaunch integrate_hq[2][2];
+  // 'auto' through the hand-over queue (S <= kHandMaxS): the DOPRI5 kernel, [beside][traj][nt]
+  // (beside: its register budget leaves room for the BDF kernel on the same SIMDs), and the
+  // BDF kernel, [traj][nt]
+  HandQLaunch integrate_hq[2][2][2];
   HandQLaunch bdf_hq[2][2];
   MHLaunch mh[kMethods];
   MHLaunch mh_init[kMethods];  // the a-priori pass (MHArgs::init)
@@ -81,9 +82,9 @@ template <class M, bool NT>
 void launch_dopri5_piped(const DevProblem& pb, const IntegrateArgs& ia, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_integrate_dopri5_piped<M, NT>), g, b, 0, s, pb, ia);
 }
-template <class M, bool TRAJ, bool NT>
+template <class M, bool TRAJ, bool NT, bool MIX>
 void launch_integrate_hq(const DevProblem& pb, const IntegrateArgs& ia, const HandQ& q, dim3 g, dim3 b, hipStream_t s) {
-  hipLaunchKernelGGL((k_integrate_hq<M, TRAJ, NT>), g, b, 0, s, pb, ia, q);
+  hipLaunchKernelGGL((k_integrate_hq<M, TRAJ, NT, MIX>), g, b, 0, s, pb, ia, q);
 }
 template <class M, bool TRAJ, bool NT>
 void launch_bdf_hq(const DevProblem& pb, const IntegrateArgs& ia, const HandQ& q, dim3 g, dim3 b, hipStream_t s) {
@@ -180,9 +181,12 @@ Entry make_entry(int32_t model_id) {
   }
   if constexpr (M::S <= kStiffRegS) fill_method<M, kBdf>(e);
   if constexpr (M::S <= kHandMaxS) {
-    e.integrate_hq[0][0] = e.integrate_hq[0][1] = launch_integrate_hq<M, false, false>;
-    e.integrate_hq[1][0] = launch_integrate_hq<M, true, false>;
-    e.integrate_hq[1][1] = launch_integrate_hq<M, true, true>;
+    e.integrate_hq[1][0][0] = e.integrate_hq[1][0][1] = launch_integrate_hq<M, false, false, true>;
+    e.integrate_hq[1][1][0] = launch_integrate_hq<M, true, false, true>;
+    e.integrate_hq[1][1][1] = launch_integrate_hq<M, true, true, true>;
+    e.integrate_hq[0][0][0] = e.integrate_hq[0][0][1] = launch_integrate_hq<M, false, false, false>;
+    e.integrate_hq[0][1][0] = launch_integrate_hq<M, true, false, false>;
+    e.integrate_hq[0][1][1] = launch_integrate_hq<M, true, true, false>;
     e.bdf_hq[0][0] = e.bdf_hq[0][1] = launch_bdf_hq<M, false, false>;
     e.bdf_hq[1][0] = launch_bdf_hq<M, true, false>;
     e.bdf_hq[1][1] = launch_bdf_hq<M, true, true>;

@@ -731,7 +731,7 @@ __device__ __forceinline__ void hand_push(const HandQ& q, const double (&y)[S], 
 // PIPE (trajectory mode, S <= 8, k_integrate_dopri5_piped): the rows go through *pp to the
 // store wave (same values, same minimum), the compute wave only evaluates observed rows.
 template <class M, int PMAX, bool TRAJ, bool NT, bool AUTO = false, bool SLOW_REDO = false, bool RESUME = false,
-          bool PIPE = false, bool QUEUE = false>
+          bool PIPE = false, bool QUEUE = false, bool MIX = false>
 __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&y)[M::S],
                                                  const double (&p)[PMAX], double* traj,
                                                  int64_t W, uint32_t off, bool active, Acc& a,
@@ -756,7 +756,7 @@ __device__ __forceinline__ bool integrate_dopri5(const DevProblem& pb, double (&
   bool dead = !active;  // dead lanes never enter the wave norm
   bool handed = false;  // RESUME: this lane was handed over to BDF
   double t = t0;
-  const Tab tb = load_tab<TRAJ && (M::S <= 8), QUEUE && OE_HQ_MIX>();
+  const Tab tb = load_tab<TRAJ && (M::S <= 8), MIX && OE_HQ_MIX>();
   double k1[S], k2[S], k3[S], k4[S], k5[S], k6[S], k7[S], yt[S], yn[S];
   M::rhs(y, t, p, k1);
 
@@ -1277,7 +1277,11 @@ __global__ void __launch_bounds__(256)
 // stream, runs the per-lane BDF pass of each handed walker from its hand-over state.
 // Together: k_integrate<M, auto, TRAJ, NT>'s outputs, bit for bit.
 // ---------------------------------------------------------------------------------
-template <class M, bool TRAJ, bool NT>
+// MIX: the tableau's e / d / c coefficients as SGPR immediates (load_tab MIX), ~200 registers
+// for the co-residency budget when k_bdf_hq runs beside it; without (k_bdf_hq after it) every
+// coefficient in VGPRs as k_integrate<M, DOPRI5>: the immediates cost the DOPRI5 step 2 s_mov
+// per use (C2: SALU 2.70e7 -> 4.09e7 per dispatch, profiles/r06/pmc).
+template <class M, bool TRAJ, bool NT, bool MIX>
 __global__ void __launch_bounds__(256) k_integrate_hq(const DevProblem pb, const IntegrateArgs ia, const HandQ hq) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
@@ -1298,7 +1302,7 @@ __global__ void __launch_bounds__(256) k_integrate_hq(const DevProblem pb, const
 #pragma unroll
   for (int j = 0; j < PMAX; ++j) p[j] = (j < pb.P) ? ia.theta[(int64_t)j * W + w] : 0.0;
   Acc a = acc_init();
-  const bool handed = integrate_dopri5<M, PMAX, TRAJ, NT, true, false, true, false, true>(
+  const bool handed = integrate_dopri5<M, PMAX, TRAJ, NT, true, false, true, false, true, MIX>(
       pb, y, p, ia.traj, W, (uint32_t)w * 8u, active, a, nullptr, nullptr, &hq);
   if (active && !handed) {
     if (ia.chi) ia.chi[w] = a.nvalid ? a.chi : __builtin_nan("");

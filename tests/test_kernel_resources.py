@@ -151,7 +151,7 @@ def test_hand_over_queue_co_residency_budget(resources):
         return (v + 7) // 8 * 8
     ks = resources["inst_two_i.hip"]
     for traj in ("ELb0ELb0E", "ELb1ELb0E", "ELb1ELb1E"):
-        prod = _find(ks, "k_integrate_hqINS_4TwoI" + traj)
+        prod = _find(ks, "k_integrate_hqINS_4TwoI" + traj + "Lb1E")  # MIX: the beside variant
         cons = _find(ks, "k_bdf_hqINS_4TwoI" + traj)
         assert alloc(prod) + alloc(cons) <= 512, (traj, prod, cons)
 
