@@ -1351,12 +1351,16 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
         ta.m.it0 = r0;
         ta.depth = std::min(depth, m.it1 - r0);
         ta.n_lanes = ((int64_t(1) << ta.depth) - 1) * W;
-        const dim3 tgrid((unsigned)((ta.n_lanes * lanes_per_walker + kBlock - 1) / kBlock));
+        // few lanes (<= one wave per SIMD): one lane per wave (MHTreeArgs::spread)
+        ta.spread = (!split && OE_MH_SPREAD && ta.n_lanes <= 4 * (int64_t)c->n_cu) ? 1 : 0;
+        const dim3 tgrid = ta.spread ? dim3((unsigned)ta.n_lanes)
+                                     : dim3((unsigned)((ta.n_lanes * lanes_per_walker + kBlock - 1) / kBlock));
+        const dim3 tblock = ta.spread ? dim3(64) : block;
         if (split) {
-          e->mh_split_tree(c->dp, ta, tgrid, block, c->stream);
+          e->mh_split_tree(c->dp, ta, tgrid, tblock, c->stream);
           OE_HIP(c, hipGetLastError());
         } else {
-          OE_HIP(c, launch_mh_tree_entry(e, c->method, c->dp, ta, tgrid, block, c->stream));
+          OE_HIP(c, launch_mh_tree_entry(e, c->method, c->dp, ta, tgrid, tblock, c->stream));
         }
         // one wave per chain pays off for deep trees of few chains (32 chains, d = 11: 0.0311 ->
         // 0.0287 ms per iteration); shallow trees of many chains keep one lane per chain

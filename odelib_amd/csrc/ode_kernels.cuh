@@ -1786,6 +1786,9 @@ __device__ __forceinline__ T uopaque(T v) {
 // speculating.  k_mh's loop around the per-lane DOPRI5 + BDF passes held ~160-380 SGPRs
 // spilled to VGPR lanes (the regime of round 4's unexplained code-shape failures; DESIGN.md
 // §3.6), where the loop-free tree kernel holds ~20; a round costs two launches.
+#ifndef OE_MH_SPREAD  // measurement builds: 0 = MH rounds never spread one lane per wave
+#define OE_MH_SPREAD 1
+#endif
 template <class M, int METHOD>
 constexpr bool kMhRoundsOnly = (METHOD == kAuto || METHOD == kBdf) && M::S <= kStiffRegS;
 
@@ -1973,6 +1976,7 @@ struct MHTreeArgs {
   double* node_chi;    // [n][W] chi of the proposal (NaN if no observation was finite)
   double* node_ss;     // [n][W] R² residual
   int32_t* node_st;    // [n][W] status bits
+  int32_t spread;      // 1: one lane per wave (lane 0 of 64-thread workgroups; few lanes, idle device)
 };
 
 template <class M, int METHOD>
@@ -1987,8 +1991,12 @@ __global__ void __launch_bounds__(256)
   const MHArgs& ma = ta.m;
   const int64_t W = ma.W;
   const int P = pb.P;
-  const int64_t gl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = gl < ta.n_lanes;
+  // spread: each lane alone in its wave (lane 0 of a 64-thread workgroup).  With few lanes
+  // (sequential rounds of a small ensemble) the device is idle anyway, and a wave then costs
+  // its own lane's DOPRI5 + BDF passes instead of its slowest DOPRI5 lane's plus its slowest
+  // BDF lane's, at a uniform wave's pace per step (1.3-1.4x for mixed waves).
+  const int64_t gl = ta.spread ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = gl < ta.n_lanes && (!ta.spread || threadIdx.x == 0);
   const int64_t gw = active ? gl : ta.n_lanes - 1;
   // 'auto': chain-major lanes — a wave holds consecutive nodes of one chain, near-identical
   // proposals that step alike, observe together at little cost and share the BDF pass's
