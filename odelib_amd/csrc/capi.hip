@@ -1351,8 +1351,10 @@ int oe_mh_run(oe_ctx* c, const oe_mh_args* a, uint32_t flags) {
         ta.m.it0 = r0;
         ta.depth = std::min(depth, m.it1 - r0);
         ta.n_lanes = ((int64_t(1) << ta.depth) - 1) * W;
-        // few lanes (<= one wave per SIMD): one lane per wave (MHTreeArgs::spread)
-        ta.spread = (!split && OE_MH_SPREAD && ta.n_lanes <= 4 * (int64_t)c->n_cu) ? 1 : 0;
+        // few lanes (<= one per CU): one lane per wave (MHTreeArgs::spread).  The notebook fit's 32
+        // chains, sequential: 1.42 -> 0.80 s; 1 024 synthetic chains (one wave per SIMD) ran
+        // slower spread, 0.27 -> 0.45 s (profiles/NOTES.md round 6)
+        ta.spread = (!split && OE_MH_SPREAD && ta.n_lanes <= (int64_t)c->n_cu) ? 1 : 0;
         const dim3 tgrid = ta.spread ? dim3((unsigned)ta.n_lanes)
                                      : dim3((unsigned)((ta.n_lanes * lanes_per_walker + kBlock - 1) / kBlock));
         const dim3 tblock = ta.spread ? dim3(64) : block;
