@@ -1031,9 +1031,15 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
       }
       e->integrate_hq[beside ? 1 : 0][tj][nj](c->dp, ia, q, grid, block, c->stream);
       OE_HIP(c, hipGetLastError());
-      // one wave per walker (slots dealt statically, k_bdf_hq): beside the DOPRI5 kernel up to
-      // kHandBdfWaves, after it one wave per SIMD (a round of dispatch when nothing was handed)
-      const int64_t G = std::min<int64_t>(beside ? (int64_t)kHandBdfWaves : 4 * (int64_t)c->n_cu, W);
+      // one-wave workgroups, slots dealt statically (k_bdf_hq): one slot per lane of the launch,
+      // so the grid covers W slots — beside the DOPRI5 kernel min(W, kHandBdfWaves) waves (W <=
+      // 16 per CU there), after it one wave per SIMD, more only past 64 per SIMD (a round of
+      // dispatch when nothing was handed).  (One 4-wave workgroup per CU, a lone stiff walker
+      // per CU, measured no faster: C2 + 0.1 % stiff 2.37 vs 2.34 ms, profiles/r06/r06y_*.)
+      const int64_t G = beside ? std::min<int64_t>((int64_t)kHandBdfWaves, W)
+                               : std::max<int64_t>(4 * (int64_t)c->n_cu, (W + 63) / 64);
+      static_assert((int64_t)kHandBdfWaves * 64 >= (int64_t)OE_HQ_MAX_W_PER_CU * 1024,
+                    "beside the DOPRI5 kernel, the BDF kernel's lanes cover every walker (n_CU <= 1024)");
       e->bdf_hq[tj][nj](c->dp, ia, q, dim3((unsigned)G), dim3(64), bs);
       OE_HIP(c, hipGetLastError());
       if (beside) {

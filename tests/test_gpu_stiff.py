@@ -114,6 +114,27 @@ def test_auto_hand_over_queue_many_walkers_bitwise(W, trajectory):
     assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == lanes
 
 
+def test_auto_hand_over_queue_more_handed_walkers_than_one_lane_each():
+    """81 920 walkers, every one stiff (tau = 1e3): more handed walkers than the BDF kernel
+    has lanes in one round of its waves (65 536 at one 4-wave workgroup per CU), so the grid
+    must cover every slot.  Every walker comes back from the BDF pass (status STIFF, finite
+    chi), and three aligned lockstep groups — first, middle, last — are the C restatement's
+    bits (a DOPRI5 walker's bits depend on its 64-walker group only)."""
+    W = 81920
+    m = product_model("two_i", method="auto")
+    theta = walker_thetas("two_i", W, seed=9).T.copy()
+    theta[4, :] = 1e3
+    y0, out = _run(m, theta, trajectory=False)
+    assert np.all(out["status"] & 8), np.count_nonzero((out["status"] & 8) == 0)
+    assert np.all(np.isfinite(out["chi"]))
+    for a in (0, W // 2, W - 64):
+        sl = slice(a, a + 64)
+        ref = rk_ref.integrate(m.fit_problem(), y0[:, sl], np.ascontiguousarray(theta[:, sl]), trajectory=False)
+        assert np.array_equal(out["status"][sl], ref["status"]), a
+        np.testing.assert_allclose(out["chi"][sl], ref["chi"], rtol=1e-12, err_msg=str(a))
+        np.testing.assert_allclose(out["ssres"][sl], ref["ssres"], rtol=1e-12, err_msg=str(a))
+
+
 @pytest.mark.parametrize("method", ["rosenbrock", "bdf"])
 @pytest.mark.parametrize("name", ["zero_i", "one_i"])
 def test_rosenbrock_other_models_bitwise(name, method):
