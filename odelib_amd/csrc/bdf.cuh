@@ -233,14 +233,26 @@ struct DTab {
   __device__ __forceinline__ double& operator()(int r, int s) const { return p[(r * S + s) * LD]; }
 #endif
 };
-// LD: columns of the table = threads of the workgroup (kMhBlock; 64 in k_bdf_hq)
+// LD = 0: the table in registers (a kernel with the registers to spare: k_bdf_hq after the
+// DOPRI5 kernel, one walker per wave — no LDS round trip in the predictor and the update)
+template <int S>
+struct DTab<S, 0> {
+  double v[bdfl::kRows * S];
+  __device__ __forceinline__ double& operator()(int r, int s) { return v[r * S + s]; }
+  __device__ __forceinline__ double operator()(int r, int s) const { return v[r * S + s]; }
+};
+// LD: columns of the table = threads of the workgroup (kMhBlock; 64 in k_bdf_hq beside)
 template <int S, int LD = kMhBlock>
 __device__ __forceinline__ DTab<S, LD> dtab_column() {
 #if OE_BDF_D_REGS
   return DTab<S, LD>{};
 #else
-  __shared__ double tab[bdfl::kRows * S * LD];
-  return DTab<S, LD>{tab + threadIdx.x};
+  if constexpr (LD == 0) {
+    return DTab<S, 0>{};
+  } else {
+    __shared__ double tab[bdfl::kRows * S * LD];
+    return DTab<S, LD>{tab + threadIdx.x};
+  }
 #endif
 }
 

@@ -1040,7 +1040,7 @@ int oe_integrate(oe_ctx* c, int64_t W, const double* y0, const double* theta, do
                                : std::max<int64_t>(4 * (int64_t)c->n_cu, (W + 63) / 64);
       static_assert((int64_t)kHandBdfWaves * 64 >= (int64_t)OE_HQ_MAX_W_PER_CU * 1024,
                     "beside the DOPRI5 kernel, the BDF kernel's lanes cover every walker (n_CU <= 1024)");
-      e->bdf_hq[tj][nj](c->dp, ia, q, dim3((unsigned)G), dim3(64), bs);
+      e->bdf_hq[beside ? 1 : 0][tj][nj](c->dp, ia, q, dim3((unsigned)G), dim3(64), bs);
       OE_HIP(c, hipGetLastError());
       if (beside) {
         OE_HIP(c, hipEventRecord(c->ev_hq[1], c->hq_stream));

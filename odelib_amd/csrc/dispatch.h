@@ -31,9 +31,9 @@ struct Entry {
   IntegrateLaunch dopri5_piped[2];  // [nt]: DOPRI5 trajectories through store waves; null when S > 6
   // 'auto' through the hand-over queue (S <= kHandMaxS): the DOPRI5 kernel, [beside][traj][nt]
   // (beside: its register budget leaves room for the BDF kernel on the same SIMDs), and the
-  // BDF kernel, [traj][nt]
+  // BDF kernel, [beside][traj][nt] (after the DOPRI5 kernel: its difference table in registers)
   HandQLaunch integrate_hq[2][2][2];
-  HandQLaunch bdf_hq[2][2];
+  HandQLaunch bdf_hq[2][2][2];  // [beside][traj][nt]
   MHLaunch mh[kMethods];
   MHLaunch mh_init[kMethods];  // the a-priori pass (MHArgs::init)
   MHTreeLaunch mh_tree[kMethods];  // speculative MH rounds (k_mh_tree); the resolve kernel is shared
@@ -86,9 +86,9 @@ template <class M, bool TRAJ, bool NT, bool MIX>
 void launch_integrate_hq(const DevProblem& pb, const IntegrateArgs& ia, const HandQ& q, dim3 g, dim3 b, hipStream_t s) {
   hipLaunchKernelGGL((k_integrate_hq<M, TRAJ, NT, MIX>), g, b, 0, s, pb, ia, q);
 }
-template <class M, bool TRAJ, bool NT>
+template <class M, bool TRAJ, bool NT, bool DREG>
 void launch_bdf_hq(const DevProblem& pb, const IntegrateArgs& ia, const HandQ& q, dim3 g, dim3 b, hipStream_t s) {
-  hipLaunchKernelGGL((k_bdf_hq<M, TRAJ, NT>), g, b, 0, s, pb, ia, q);
+  hipLaunchKernelGGL((k_bdf_hq<M, TRAJ, NT, DREG>), g, b, 0, s, pb, ia, q);
 }
 template <class M, int METHOD, bool INIT = false>
 void launch_mh(const DevProblem& pb, const MHArgs& ma, dim3 g, dim3 b, hipStream_t s) {
@@ -187,9 +187,12 @@ Entry make_entry(int32_t model_id) {
     e.integrate_hq[0][0][0] = e.integrate_hq[0][0][1] = launch_integrate_hq<M, false, false, false>;
     e.integrate_hq[0][1][0] = launch_integrate_hq<M, true, false, false>;
     e.integrate_hq[0][1][1] = launch_integrate_hq<M, true, true, false>;
-    e.bdf_hq[0][0] = e.bdf_hq[0][1] = launch_bdf_hq<M, false, false>;
-    e.bdf_hq[1][0] = launch_bdf_hq<M, true, false>;
-    e.bdf_hq[1][1] = launch_bdf_hq<M, true, true>;
+    e.bdf_hq[1][0][0] = e.bdf_hq[1][0][1] = launch_bdf_hq<M, false, false, false>;
+    e.bdf_hq[1][1][0] = launch_bdf_hq<M, true, false, false>;
+    e.bdf_hq[1][1][1] = launch_bdf_hq<M, true, true, false>;
+    e.bdf_hq[0][0][0] = e.bdf_hq[0][0][1] = launch_bdf_hq<M, false, false, true>;
+    e.bdf_hq[0][1][0] = launch_bdf_hq<M, true, false, true>;
+    e.bdf_hq[0][1][1] = launch_bdf_hq<M, true, true, true>;
   }
   if constexpr (M::S <= 8 && dp_pipe_slots<M::S>() >= 2) {  // a slot ring of >= 2 steps fits (S <= 6)
     e.dopri5_piped[0] = launch_dopri5_piped<M, false>;

@@ -1328,7 +1328,9 @@ constexpr int kHandBdfWaves = OE_HQ_WAVES;  // k_bdf_hq workgroups at most (one 
 // every producer wave is done without reaching it; no loop runs around the BDF pass, so the
 // pass's loop-invariant constants are formed after the wait instead of in the prologue, where
 // they lived across the polling in SGPRs spilled to VGPR lanes (111 spilled SGPRs -> 21).
-template <class M, bool TRAJ, bool NT>
+// DREG (after the DOPRI5 kernel): the BDF pass's difference table in registers (DTab<S, 0>);
+// beside it the table stays in LDS, within the co-residency budget.
+template <class M, bool TRAJ, bool NT, bool DREG = false>
 __global__ void __launch_bounds__(64) k_bdf_hq(const DevProblem pb, const IntegrateArgs ia, const HandQ hq) {
   constexpr int S = M::S;
   constexpr int PMAX = kPmax<M>;
@@ -1379,7 +1381,7 @@ __global__ void __launch_bounds__(64) k_bdf_hq(const DevProblem pb, const Integr
   // wave sharing its SIMD is issue-bound.  At a higher priority the BDF wave issues whenever
   // it is ready, taking few slots from the DOPRI5 wave, instead of waiting behind it.
   if (OE_HQ_PRIO) __builtin_amdgcn_s_setprio(3);
-  integrate_bdf_lane<M, PMAX, TRAJ, NT, 64>(pb, y, t, i, k, p, ia.traj, W, w, part, part, a);
+  integrate_bdf_lane<M, PMAX, TRAJ, NT, DREG ? 0 : 64>(pb, y, t, i, k, p, ia.traj, W, w, part, part, a);
 #if OE_HQ_TRACE
   {
     // s_memrealtime: 100 MHz; chi = start·1e5 + the DOPRI5 kernel's last wave end, ssres =

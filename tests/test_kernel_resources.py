@@ -152,7 +152,7 @@ def test_hand_over_queue_co_residency_budget(resources):
     ks = resources["inst_two_i.hip"]
     for traj in ("ELb0ELb0E", "ELb1ELb0E", "ELb1ELb1E"):
         prod = _find(ks, "k_integrate_hqINS_4TwoI" + traj + "Lb1E")  # MIX: the beside variant
-        cons = _find(ks, "k_bdf_hqINS_4TwoI" + traj)
+        cons = _find(ks, "k_bdf_hqINS_4TwoI" + traj + "Lb0E")  # beside: the LDS-table variant
         assert alloc(prod) + alloc(cons) <= 512, (traj, prod, cons)
 
 
