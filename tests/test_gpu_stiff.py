@@ -114,6 +114,31 @@ def test_auto_hand_over_queue_many_walkers_bitwise(W, trajectory):
     assert sorted(np.nonzero(out["status"] & 8)[0].tolist()) == lanes
 
 
+@pytest.mark.parametrize("name,W", [("one_i", 300), ("one_i", 5000), ("chain4", 300)])
+def test_auto_hand_over_queue_other_models_bitwise(name, W):
+    """The hand-over queue's kernels for the other models it serves (S <= 4): one_i (3 states)
+    with a fast infected-cell decay (lam = 1e4) and the synthetic 4-state chain (tau = 1e4) in
+    a few lanes — beside the DOPRI5 kernel (300 walkers) and after it (5 000) — the C
+    restatement's bits, trajectories included."""
+    from helpers import chain_problem
+    if name == "chain4":
+        m = chain_problem(4, method="auto")
+        theta = walker_thetas("two_i", W, seed=2).T.copy()
+        k = 4
+    else:
+        m = product_model(name, method="auto")
+        theta = walker_thetas(name, W, seed=2).T.copy()
+        k = 3
+    lanes = [1, 64, 200, W - 1]
+    theta[k, lanes] = 1e4
+    y0, out = _run(m, theta)
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"], equal_nan=True)
+    assert np.array_equal(out["status"], ref["status"])
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
+    assert np.all(out["status"][lanes] & 8), out["status"][lanes]
+
+
 def test_auto_hand_over_queue_more_handed_walkers_than_one_lane_each():
     """81 920 walkers, every one stiff (tau = 1e3): more handed walkers than the BDF kernel
     has lanes in one round of its waves (65 536 at one 4-wave workgroup per CU), so the grid
