@@ -651,7 +651,9 @@ __device__ __forceinline__ void dp_pipe_publish(DpPipe<S>& pp, double t, double 
 // BDF pass does not depend on the lane or wave running it (profiles/NOTES.md r05o): the same
 // bits as the in-wave pass.  Measured against it (NOTES round 6, r06p; ms, 0.1 % / 1 % stiff):
 // 1 024 walkers 1.92 -> 1.61 / 2.97 -> 1.79; 4 096: 2.09 -> 1.79 / 3.17 -> 1.80; 16 384: 2.35 ->
-// 2.19 / 3.09 -> 2.22; 65 536 (C2): 2.49 -> 2.37 / 2.85 -> 2.87; none stiff: within 0.05 ms.
+// 2.19 / 3.09 -> 2.22; 65 536 (C2): 2.49 -> 2.37 / 2.85 -> 2.87; none stiff: within 0.05 ms
+// (after the DOPRI5 kernel the difference table then went to registers: C2 2.33 -> 2.26 / 2.86
+// -> 2.77, r06z3).
 // Rejected on the way: BDF waves inside the DOPRI5 workgroups (every wave then gets 256
 // registers; BDF steps ~1.5x slower), the BDF kernel beside the DOPRI5 kernel for large
 // ensembles (each BDF wave shares a SIMD with an issue-bound DOPRI5 wave: C2 + 1 % stiff
@@ -1320,9 +1322,10 @@ __global__ void __launch_bounds__(256) k_integrate_hq(const DevProblem pb, const
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(hq.ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr int kHandBdfWaves = OE_HQ_WAVES;  // k_bdf_hq workgroups at most (one wave each)
-// Slots are dealt statically: BDF wave g's lane l takes slot g + l·G (G = the kernel's waves),
-// so each handed walker is alone in its wave while there are no more than G of them, and no
+constexpr int kHandBdfWaves = OE_HQ_WAVES;  // k_bdf_hq's one-wave workgroups beside the DOPRI5 kernel, at most
+// Slots are dealt statically: BDF wave g's lane l takes slot g + l·G (G = the kernel's waves;
+// the host sizes G·64 >= W, so every slot has a lane: capi.hip oe_integrate), so each handed
+// walker is alone in its wave while there are no more than G of them, and no
 // wave claims anything (a CAS claim by a thousand waves on one counter serialised the claims:
 // 655 walkers were picked up over 6.7 ms, r06n).  A lane waits until its slot is published or
 // every producer wave is done without reaching it; no loop runs around the BDF pass, so the
