@@ -858,3 +858,40 @@ def test_tuned_choice_is_shared_by_contexts_on_the_device():
     assert dt < 0.05, dt  # one launch, no tuning (the settle alone is >= 60 ms of launches)
     r1 = e1.integrate(y0, theta, kernel="direct")
     assert np.array_equal(r2["traj"].cpu().numpy(), r1["traj"].cpu().numpy())
+
+
+def test_c_abi_error_codes_leave_the_context_usable():
+    """The boundary's error behaviour (include/odelib_amd.h, INTEGRATION.md "Error behaviour"):
+    a call before oe_problem_set is OE_ERR_STATE, walker counts outside [1, 2^29], a missing y0
+    and a one-point time grid are OE_ERR_ARG, each with a message naming the entry point — and
+    the context then integrates as if nothing had happened (the device path's bits)."""
+    import ctypes as C
+    m = _model("two_i", "dopri5")
+    W = 64
+    theta = np.ascontiguousarray(_walkers("two_i", W))
+    y0 = np.ascontiguousarray(np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1))
+    fp = m.fit_problem()
+    ptr = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+    chi = np.full(W, -1.0)
+    ctx = N.Context(0)
+    try:
+        with pytest.raises(RuntimeError, match=r"oe_integrate failed \(-3\)"):
+            ctx.integrate(W, ptr(y0), ptr(theta), None, ptr(chi), None, None, N.OE_HOST_PTRS)
+        prob = fp.to_c()
+        ctx.problem_set(prob)
+        for bad_w in (0, -5, (1 << 29) + 1):
+            with pytest.raises(RuntimeError, match=r"oe_integrate failed \(-1\).*n_walkers"):
+                ctx.integrate(bad_w, ptr(y0), ptr(theta), None, ptr(chi), None, None, N.OE_HOST_PTRS)
+        with pytest.raises(RuntimeError, match=r"oe_integrate failed \(-1\).*y0"):
+            ctx.integrate(W, None, ptr(theta), None, ptr(chi), None, None, N.OE_HOST_PTRS)
+        assert np.all(chi == -1.0)  # nothing was written
+        bad = fp.to_c()
+        bad.n_times = 1
+        with pytest.raises(RuntimeError, match=r"oe_problem_set failed \(-1\)"):
+            ctx.problem_set(bad)
+        ctx.problem_set(prob)
+        ctx.integrate(W, ptr(y0), ptr(theta), None, ptr(chi), None, None, N.OE_HOST_PTRS)
+    finally:
+        ctx.close()
+    dev = m.engine().integrate(y0, theta)
+    assert np.array_equal(chi, dev["chi"].cpu().numpy(), equal_nan=True)
