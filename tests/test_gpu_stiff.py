@@ -392,3 +392,20 @@ def test_bdf_refused_above_register_path():
     with pytest.raises(N.NativeUnsupported):
         chain_problem(10, method="bdf").engine()
     chain_problem(6, method="bdf").engine()
+
+
+@pytest.mark.parametrize("method", ["rk4", "dopri5", "auto", "bdf", "rosenbrock"])
+def test_two_point_time_grid_bitwise(method):
+    """The smallest grid the ABI takes (T = 2: the initial state and one output row; every
+    look-ahead load then reads the +inf sentinels): every method, stiff lanes included, the C
+    restatement's bits."""
+    from helpers import chain_problem
+    m = chain_problem(4, method=method, T=2)
+    W = 70
+    theta = _mixed_thetas("two_i", W, [3, 64, 69])
+    y0, out = _run(m, theta)
+    assert out["traj"].shape[0] == 2
+    ref = rk_ref.integrate(m.fit_problem(), y0, theta)
+    assert np.array_equal(out["traj"], ref["traj"], equal_nan=True)
+    assert np.array_equal(out["status"], ref["status"])
+    np.testing.assert_allclose(out["chi"], ref["chi"], rtol=1e-12)
