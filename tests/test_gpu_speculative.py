@@ -235,3 +235,24 @@ def test_speculative_rounds_with_stiff_proposals_vs_c_restatement(method):
     for k in ("samples", "theta", "final"):
         np.testing.assert_allclose(dev[k], ref[k], rtol=1e-8, err_msg=k)
     assert np.array_equal(dev["status"], ref["status"])
+
+
+@pytest.mark.parametrize("method", ["rk4", "dopri5", "auto"])
+@pytest.mark.parametrize("nits", [2, 3])
+def test_smallest_mh_runs_on_a_two_point_grid(method, nits):
+    """The smallest runs the ABI takes: one or two MH iterations (nits = 2, 3), one and three
+    chains, on a two-point time grid — speculative rounds (a round then covers at most the
+    iterations left) give the sequential chains bit for bit, every chain's chi finite."""
+    from helpers import chain_problem
+    m = chain_problem(4, method=method, T=2)
+    P = len(m.get_pnames())
+    for W in (1, 3):
+        theta = np.repeat(np.array([float(m.parameters[p].val) for p in m.get_pnames()])[:, None], W, axis=1)
+        y0 = np.repeat(np.asarray(m.get_inits(), float)[:, None], W, axis=1)
+        kw = dict(nits=nits, burnin=0, walk_mask=np.ones(P, np.uint8), rng="philox", seed=3)
+        eng = m.engine()
+        seq = _np(eng.mh_run(theta, y0, **kw))
+        spec = _np(eng.mh_run(theta, y0, speculate="auto", **kw))
+        _equal(spec, seq)
+        assert seq["samples"].shape[0] == nits - 1
+        assert np.all(np.isfinite(seq["final"][0]))
